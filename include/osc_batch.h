@@ -1,0 +1,136 @@
+/*
+ * osc_batch.h -- C-ABI of the MI355X-native batched operational-space-control (OSC) solver.
+ *
+ * One call solves, for every environment of a batch, the per-tick OSC quadratic program of
+ * vannem95/operational-space-control and returns the joint torques.  The entry points replace
+ * the reference's per-tick inner operator boundary (paths relative to the reference's
+ * operational-space-control/ directory):
+ *
+ *   osc_desc_from_yaml / osc_model_create
+ *       replace the build-time CasADi generation of the six QP functions and the constexpr
+ *       sizes: unitree_go2/autogen/autogen.py:19-56 (YAML + sizes), :240-411 (codegen), and the
+ *       hard-coded bound vectors unitree_go2/operational_space_controller.h:276-309
+ *       (walter_sr/operational_space_controller.h:309-353).
+ *   osc_batch_solve
+ *       replaces, per environment, the six CasADi evaluations
+ *       (unitree_go2/operational_space_controller.h:457-481 via unitree_go2/utilities.h:43-77:
+ *        int F(const double** arg, double** res, casadi_int* iw, double* w, int mem) for
+ *        F in {beq, Aeq, bineq, Aineq, H, f}), the OSQP stacking/update
+ *       (operational_space_controller.h:483-529: UpdateObjectiveAndConstraintMatrices,
+ *        SetObjectiveVector, SetBounds, Init, SetWarmStart), the solve
+ *       (operational_space_controller.h:531-536: OsqpSolver::Solve, primal_solution,
+ *        dual_solution) and the torque slice (operational_space_controller.h:573).
+ *   osc_model_destroy
+ *       replaces the teardown of the OSQP workspace / CasADi memory pools.
+ *
+ * Inputs are what update_osc_data (operational_space_controller.h:376-455) produces, batched
+ * env-major, row-major per environment, IEEE fp64:
+ *   M    [nenv][nv][nv]      mass matrix (mj_fullM)
+ *   C    [nenv][nv]          bias forces (qfrc_bias)
+ *   J    [nenv][6*ns][nv]    task Jacobian [Jp_0..Jp_{ns-1}; Jr_0..Jr_{ns-1}]
+ *   b    [nenv][6*ns]        task bias acceleration  Jdot * qd
+ *   T    [nenv][ns][6]       task-space acceleration targets (TaskspaceTargets, row-major)
+ *   mask [nenv][nc]          contact mask (State::contact_mask)
+ * The contact Jacobian is NOT an input: as in the reference it is the last 3*nc translational
+ * rows of J, transposed (operational_space_controller.h:439-445).
+ *
+ * Outputs:
+ *   tau    [nenv][nu]             torque command = x[nv : nv+nu]
+ *   x      [nenv][nv+nu+3nc]      (nullable) full design vector (dv, u, z) = get_solution()
+ *   status [nenv]                 (nullable) OSC_SOLVE_* code per environment
+ *   iters  [nenv]                 (nullable) interior-point iterations used
+ *
+ * All batch pointers passed to osc_batch_solve are DEVICE pointers (HBM-resident); `stream` is
+ * a hipStream_t (NULL = default stream).  The call is asynchronous with respect to the host.
+ * Every function returns an osc_status (0 = OK).  Handles are re-entrant: a model may be used
+ * from several streams concurrently; there is no global state.
+ */
+#ifndef OSC_BATCH_H_
+#define OSC_BATCH_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OSC_ABI_VERSION 1
+#define OSC_MAX_SITES 32
+#define OSC_MAX_NU 16
+
+/* Return codes (map onto the reference's absl::Status use: InternalError for load failures,
+ * FailedPreconditionError for lifecycle misuse -- operational_space_controller.h:112-218). */
+typedef enum {
+  OSC_OK = 0,
+  OSC_ERR_INVALID_ARGUMENT = 1,   /* null pointer, nenv < 0, inconsistent descriptor        */
+  OSC_ERR_UNSUPPORTED_DIMS = 2,   /* (nv, nu, nc, ns) has no compiled gfx950 kernel          */
+  OSC_ERR_IO = 3,                 /* YAML file missing / unreadable / malformed               */
+  OSC_ERR_DEVICE = 4,             /* HIP runtime error (allocation, launch)                   */
+  OSC_ERR_NO_DEVICE = 5           /* no HIP device visible                                    */
+} osc_status;
+
+/* Per-environment solve status written to status[] */
+typedef enum {
+  OSC_SOLVE_OK = 0,               /* converged: complementarity <= eps_mu                     */
+  OSC_SOLVE_MAX_ITER = 1,         /* iteration cap reached; best iterate returned             */
+  OSC_SOLVE_NUMERICAL = 2         /* non-finite values encountered (e.g. NaN inputs)         */
+} osc_solve_status;
+
+/* Everything that defines the QP of one robot -- what autogen.py bakes into generated C
+ * (sizes, weights, friction) plus the bound vectors hard-coded in the controller header. */
+typedef struct {
+  int32_t nv;                     /* generalized velocities (mjModel::nv)                    */
+  int32_t nu;                     /* actuators; B = [0_{(nv-nu) x nu}; I_nu]                  */
+  int32_t nc;                     /* contact sites (last nc of the ns sites)                  */
+  int32_t ns;                     /* task sites (noncontact + contact)                        */
+  double mu;                      /* friction_coefficient                                     */
+  double w_pos[OSC_MAX_SITES];    /* <site>_translational_tracking, site order                */
+  double w_rot[OSC_MAX_SITES];    /* <site>_rotational_tracking                               */
+  double w_torque;                /* weights_config.torque                                    */
+  double w_reg;                   /* weights_config.regularization                            */
+  double u_lb[OSC_MAX_NU];        /* torque bounds (osc.h:285-296)                            */
+  double u_ub[OSC_MAX_NU];
+  double z_lb[3];                 /* per-contact force bounds before the mask multiply        */
+  double z_ub[3];                 /*   (osc.h:297-308): {-inf,-inf,0} / {inf,inf,big_number}  */
+  double infinity;                /* OSQP_INFTY (1e30); |bound| >= infinity/1e10 = no bound   */
+  double eps_mu;                  /* interior-point stop: mean complementarity <= eps_mu      */
+  int32_t max_iter;               /* interior-point iteration cap                             */
+} osc_model_desc;
+
+typedef struct osc_model osc_model;   /* opaque: descriptor + device-resident parameters */
+
+/* Host-only: fill `desc` for `robot` ("unitree_go2", "walter_sr", "walter_sr_wheels") from a
+ * YAML file in the reference's config schema (config/<robot>/<robot>_config.yaml).  Needs no
+ * GPU.  `yaml_path` NULL = the robot's default config next to the library. */
+int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_model_desc* desc);
+
+/* Validate `desc`, pick the compiled kernel for its dimensions and upload its parameters to
+ * the current HIP device. */
+int osc_model_create(const osc_model_desc* desc, osc_model** out);
+
+/* Convenience: osc_desc_from_yaml + osc_model_create. */
+int osc_model_create_from_yaml(const char* robot, const char* yaml_path, osc_model** out);
+
+int osc_model_destroy(osc_model* model);
+
+/* Copy of the descriptor a model was created from. */
+int osc_model_get_desc(const osc_model* model, osc_model_desc* desc);
+
+/* Batched solve; see the header comment for layouts.  Device pointers, async on `stream`. */
+int osc_batch_solve(const osc_model* model, int32_t nenv,
+                    const double* M, const double* C, const double* J, const double* b,
+                    const double* T, const double* contact_mask,
+                    double* tau, double* x, int32_t* status, int32_t* iters,
+                    void* stream);
+
+/* Human-readable name of an osc_status. */
+const char* osc_status_string(int status);
+
+/* Library ABI version (OSC_ABI_VERSION). */
+int osc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OSC_BATCH_H_ */

@@ -1,0 +1,93 @@
+"""ctypes binding of the C-ABI in include/osc_batch.h (libosc_batch.so, built in-tree).
+
+This is the Python twin of the binding a maintainer would add on the reference side
+(INTEGRATION.md).  There is deliberately NO fallback: if the HIP library is missing the import
+fails, and solving on a machine without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libosc_batch.so")
+
+OSC_MAX_SITES = 32
+OSC_MAX_NU = 16
+
+STATUS_NAMES = {0: "OSC_OK", 1: "OSC_ERR_INVALID_ARGUMENT", 2: "OSC_ERR_UNSUPPORTED_DIMS",
+                3: "OSC_ERR_IO", 4: "OSC_ERR_DEVICE", 5: "OSC_ERR_NO_DEVICE"}
+SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL = 0, 1, 2
+
+EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
+                    "osc_model_destroy", "osc_model_get_desc", "osc_batch_solve",
+                    "osc_status_string", "osc_abi_version")
+
+
+class OscModelDesc(ctypes.Structure):
+    _fields_ = [
+        ("nv", ctypes.c_int32), ("nu", ctypes.c_int32), ("nc", ctypes.c_int32),
+        ("ns", ctypes.c_int32),
+        ("mu", ctypes.c_double),
+        ("w_pos", ctypes.c_double * OSC_MAX_SITES),
+        ("w_rot", ctypes.c_double * OSC_MAX_SITES),
+        ("w_torque", ctypes.c_double), ("w_reg", ctypes.c_double),
+        ("u_lb", ctypes.c_double * OSC_MAX_NU), ("u_ub", ctypes.c_double * OSC_MAX_NU),
+        ("z_lb", ctypes.c_double * 3), ("z_ub", ctypes.c_double * 3),
+        ("infinity", ctypes.c_double),
+        ("eps_mu", ctypes.c_double),
+        ("max_iter", ctypes.c_int32),
+    ]
+
+
+class OSCError(RuntimeError):
+    def __init__(self, where: str, code: int):
+        super().__init__(f"{where} failed: {STATUS_NAMES.get(code, code)}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libosc_batch.so (raises if it has not been built -- no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build() "
+                          "(hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, dp = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(OscModelDesc)
+    L.osc_desc_from_yaml.argtypes = [ctypes.c_char_p, ctypes.c_char_p, dp]
+    L.osc_desc_from_yaml.restype = ctypes.c_int
+    L.osc_model_create.argtypes = [dp, ctypes.POINTER(vp)]
+    L.osc_model_create.restype = ctypes.c_int
+    L.osc_model_create_from_yaml.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.osc_model_create_from_yaml.restype = ctypes.c_int
+    L.osc_model_destroy.argtypes = [vp]
+    L.osc_model_destroy.restype = ctypes.c_int
+    L.osc_model_get_desc.argtypes = [vp, dp]
+    L.osc_model_get_desc.restype = ctypes.c_int
+    L.osc_batch_solve.argtypes = [vp, i32] + [vp] * 10 + [vp]
+    L.osc_batch_solve.restype = ctypes.c_int
+    L.osc_status_string.argtypes = [ctypes.c_int]
+    L.osc_status_string.restype = ctypes.c_char_p
+    L.osc_abi_version.argtypes = []
+    L.osc_abi_version.restype = ctypes.c_int
+    # test hooks (not in the public header)
+    L.osc_debug_dump_size.argtypes = [vp]
+    L.osc_debug_dump_size.restype = ctypes.c_int
+    L.osc_debug_reduced_qp.argtypes = [vp, i32] + [vp] * 9
+    L.osc_debug_reduced_qp.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def desc_from_yaml(robot: str, yaml_path: str | None = None) -> OscModelDesc:
+    d = OscModelDesc()
+    rc = lib().osc_desc_from_yaml(robot.encode(), yaml_path.encode() if yaml_path else None,
+                                  ctypes.byref(d))
+    if rc != 0:
+        raise OSCError("osc_desc_from_yaml", rc)
+    return d

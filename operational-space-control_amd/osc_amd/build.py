@@ -1,0 +1,43 @@
+"""Build the in-tree native library: libosc_batch.so (HIP kernels for gfx950 + C-ABI + YAML loader).
+
+    python -m osc_amd.build          (from operational-space-control_amd/)
+
+Plain hipcc, no cmake: the library is two translation units.  The .so lands in
+operational-space-control_amd/lib/ so that it travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+OUT = os.path.join(PKG_DIR, "lib", "libosc_batch.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["osc_batch.hip", "osc_model.cpp"]
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    hdrs = [os.path.join(REPO, "include", "osc_batch.h")]
+    if not force and os.path.exists(OUT):
+        t_out = os.path.getmtime(OUT)
+        if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):
+            return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = [HIPCC, "-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result", "-I", os.path.join(REPO, "include"),
+           *srcs, "-o", OUT]
+    if verbose:
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))

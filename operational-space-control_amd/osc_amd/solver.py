@@ -1,0 +1,113 @@
+"""Host-side batched OSC solver: the reference's per-tick QP for a whole batch of environments.
+
+Reference interface this mirrors (paths relative to the reference's operational-space-control/):
+  * OperationalSpaceController(xml_path, control_rate_us, OsqpSettings)   osc.h:108
+      -> OSCBatchSolver(robot, yaml_path, eps_mu, max_iter)   (model from the same YAML schema)
+  * update_optimization_data() + update_optimization() + solve_optimization()  osc.h:457-536
+      -> OSCBatchSolver.solve(M, C, J, b, T, mask)          (all environments in one launch)
+  * get_torque_command() -> tau;  get_solution() -> x        osc.h:230-238
+  * absl::Status error convention -> OSCError with the osc_status code.
+
+Inputs are torch float64 CUDA tensors already resident in HBM (numpy arrays are copied to the
+current device for convenience).  Everything is launched through the C-ABI
+(include/osc_batch.h) on the current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+
+import numpy as np
+import torch
+
+from . import _lib
+from .robots import config_path, dims
+
+
+@dataclasses.dataclass
+class SolveResult:
+    tau: torch.Tensor          # (nenv, nu)
+    x: torch.Tensor | None     # (nenv, nv + nu + 3nc) design vector (dv, u, z)
+    status: torch.Tensor       # (nenv,) int32, 0 = converged
+    iters: torch.Tensor        # (nenv,) int32, interior-point iterations
+
+
+class OSCBatchSolver:
+    def __init__(self, robot: str, yaml_path: str | None = None, eps_mu: float | None = None,
+                 max_iter: int | None = None, device: torch.device | int | None = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("OSCBatchSolver needs a HIP device (no CPU fallback exists)")
+        self.robot = robot
+        self.dims = dims(robot)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        desc = _lib.desc_from_yaml(robot, yaml_path or config_path(robot))
+        if eps_mu is not None:
+            desc.eps_mu = float(eps_mu)
+        if max_iter is not None:
+            desc.max_iter = int(max_iter)
+        self.desc = desc
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = _lib.lib().osc_model_create(ctypes.byref(desc), ctypes.byref(h))
+        if rc != 0:
+            raise _lib.OSCError("osc_model_create", rc)
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().osc_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _as_dev(self, a, shape, name):
+        if isinstance(a, np.ndarray):
+            a = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+        if not isinstance(a, torch.Tensor):
+            raise TypeError(f"{name}: expected torch.Tensor or numpy array")
+        a = a.to(device=self.device, dtype=torch.float64).contiguous()
+        if tuple(a.shape) != shape:
+            raise ValueError(f"{name}: expected shape {shape}, got {tuple(a.shape)}")
+        return a
+
+    def alloc_outputs(self, nenv: int, want_x: bool = False):
+        d = self.dims
+        opts = dict(device=self.device)
+        tau = torch.empty((nenv, d["nu"]), dtype=torch.float64, **opts)
+        x = torch.empty((nenv, d["n"]), dtype=torch.float64, **opts) if want_x else None
+        status = torch.empty((nenv,), dtype=torch.int32, **opts)
+        iters = torch.empty((nenv,), dtype=torch.int32, **opts)
+        return SolveResult(tau, x, status, iters)
+
+    def solve_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None) -> SolveResult:
+        """Launch only (no allocation, no host sync): the benchmarked call."""
+        nenv = out.tau.shape[0]
+        s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = _lib.lib().osc_batch_solve(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
+                                        ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
+                                        ptr(out.iters), ctypes.c_void_p(s))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_solve", rc)
+        return out
+
+    def prepare(self, M, C, J, b, T, mask):
+        d = self.dims
+        nenv = int(M.shape[0])
+        return (self._as_dev(M, (nenv, d["nv"], d["nv"]), "M"),
+                self._as_dev(C, (nenv, d["nv"]), "C"),
+                self._as_dev(J, (nenv, d["s"], d["nv"]), "J"),
+                self._as_dev(b, (nenv, d["s"]), "b"),
+                self._as_dev(T, (nenv, d["ns"], 6), "T"),
+                self._as_dev(mask, (nenv, d["nc"]), "mask"))
+
+    def solve(self, M, C, J, b, T, mask, want_x: bool = False) -> SolveResult:
+        args = self.prepare(M, C, J, b, T, mask)
+        out = self.alloc_outputs(int(args[0].shape[0]), want_x)
+        with torch.cuda.device(self.device):
+            return self.solve_into(out, *args)

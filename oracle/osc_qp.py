@@ -1,0 +1,240 @@
+"""CPU oracle, part 1: the reference's per-tick OSC QP, restated in closed form (numpy, fp64).
+
+TEST INFRASTRUCTURE ONLY.  Nothing under ``oracle/`` is part of the product: only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it,
+and only as the checker.
+
+PARITY STATUS: *parity unpinned* against the reference's own outputs.  The reference has no
+tests, no golden vectors and no fixtures, and its path cannot be built or
+imported here (MuJoCo, CasADi, OSQP, Eigen, abseil absent).  This module
+restates the CasADi-generated arithmetic symbol by symbol from ``autogen.py`` and the
+stacking/bounds code of ``operational_space_controller.h``; its solutions are certified by
+KKT optimality (``qp_exact.py``) and by analytic known-answer cases (``tests/test_oracle.py``).
+
+Reference citations (paths relative to /root/reference/operational-space-control):
+  * sizes, design vector split, B matrix ........ unitree_go2/autogen/autogen.py:44-56,
+                                                   walter_sr/autogen/autogen.py:44-60
+  * equality constraints  M dv + C - B u - Jc z .. unitree_go2/autogen/autogen.py:58-89
+  * friction pyramid rows ......................... unitree_go2/autogen/autogen.py:91-129
+  * objective (tracking + torque + regularizer) .. unitree_go2/autogen/autogen.py:131-238,
+                                                   walter_sr/autogen/autogen.py:135-345
+  * beq/Aeq/bineq/Aineq/H/f as CasADi functions
+    (jacobian / hessian evaluated at x = 0) ...... unitree_go2/autogen/autogen.py:274-319
+  * design_vector is never updated (stays 0) .... unitree_go2/operational_space_controller.h:275
+  * contact Jacobian = last 3nc translational
+    rows of J, transposed ......................... unitree_go2/operational_space_controller.h:439-445
+  * OSQP stacking A=[Aeq;Aineq;I], l, u, masks .... unitree_go2/operational_space_controller.h:483-497
+  * bounds (u limits, z limits, big_number) ...... unitree_go2/operational_space_controller.h:276-309,
+                                                   walter_sr/operational_space_controller.h:309-353
+  * torque = x[nv : nv+nu] ....................... unitree_go2/operational_space_controller.h:573
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+import numpy as np
+import yaml
+
+# OSQP 0.6.3 defines OSQP_INFTY as the finite 1e30 (osqp/include/constants.h, not vendored);
+# the reference uses it for every "infinite" bound (operational_space_controller.h:276).
+OSQP_INFTY = 1e30
+# `const float big_number = 1e4;` (operational_space_controller.h:279) -- fz upper bound.
+BIG_NUMBER = float(np.float32(1e4))
+
+_PKG_CONFIG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "operational-space-control_amd", "config")
+
+# Per-robot static data.  The site "key" order is the order in which autogen.py splits the
+# task rows (vertsplit_n over sites), which is also the YAML site order.
+ROBOTS = {
+    # unitree_go2/autogen/autogen.py:160-219 (base, fr, fl, hr, hl); bounds osc.h:285-308.
+    "unitree_go2": dict(
+        nv=18, nu=12, nc=4,
+        site_keys=["base", "fr", "fl", "hr", "hl"],
+        u_lb=[-23.7, -23.7, -45.3] * 4,
+        u_ub=[23.7, 23.7, 45.3] * 4,
+        config="unitree_go2_config.yaml",
+        # dof groups touched by each site for synthetic Jacobians (floating base 0..5, 4 legs x 3)
+        site_dofs=[list(range(6))] + [list(range(6)) + list(range(6 + 3 * l, 9 + 3 * l)) for l in range(4)],
+        base_mass=15.0,
+    ),
+    # walter_sr/autogen/autogen.py:163-330; bounds walter_sr/osc.h:309-353.
+    "walter_sr": dict(
+        nv=14, nu=8, nc=8,
+        site_keys=["torso", "tls", "trs", "hls", "hrs", "tlh", "trh", "hlh", "hrh",
+                   "tlf", "tlr", "trf", "trr", "hlf", "hlr", "hrf", "hrr"],
+        u_lb=[-1000.0] * 8,
+        u_ub=[1000.0] * 8,
+        config="walter_sr_config.yaml",
+        base_mass=10.0,
+    ),
+    "walter_sr_wheels": dict(
+        nv=14, nu=8, nc=8,
+        site_keys=["torso", "tls", "trs", "hls", "hrs", "tlh", "trh", "hlh", "hrh",
+                   "tlf", "tlr", "trf", "trr", "hlf", "hlr", "hrf", "hrr"],
+        u_lb=[-1000.0] * 8,
+        u_ub=[1000.0] * 8,
+        config="walter_sr_wheels_config.yaml",
+        base_mass=10.0,
+    ),
+}
+
+
+def _walter_site_dofs():
+    # legs tl, tr, hl, hr; each leg = (thigh dof, shin dof) at 6 + 2*leg (+1).
+    base = list(range(6))
+    leg = lambda l: [6 + 2 * l, 7 + 2 * l]
+    dofs = [base]
+    dofs += [base + leg(l) for l in range(4)]            # shins: thigh + shin joints
+    dofs += [base + leg(l)[:1] for l in range(4)]        # thighs: thigh joint only
+    dofs += [base + leg(l // 2) for l in range(8)]       # wheels: 2 per leg, end of the shin
+    return dofs
+
+
+ROBOTS["walter_sr"]["site_dofs"] = _walter_site_dofs()
+ROBOTS["walter_sr_wheels"]["site_dofs"] = _walter_site_dofs()
+
+
+@dataclasses.dataclass
+class OSCModel:
+    """Everything that defines the QP for one robot (what autogen.py bakes into C)."""
+    name: str
+    nv: int
+    nu: int
+    nc: int
+    ns: int
+    mu: float
+    w_pos: np.ndarray   # (ns,) translational tracking weight per site
+    w_rot: np.ndarray   # (ns,) rotational tracking weight per site
+    w_torque: float
+    w_reg: float
+    u_lb: np.ndarray
+    u_ub: np.ndarray
+    site_dofs: list
+
+    @property
+    def nz(self):
+        return 3 * self.nc
+
+    @property
+    def n(self):          # design vector size  (autogen.py:47)
+        return self.nv + self.nu + self.nz
+
+    @property
+    def m(self):          # OSQP rows: Aeq + Aineq + identity box  (constants.h:20)
+        return self.nv + 4 * self.nc + self.n
+
+    @property
+    def s(self):          # task rows  (constants.h:13)
+        return 6 * self.ns
+
+
+def load_model(robot: str, yaml_path: str | None = None) -> OSCModel:
+    r = ROBOTS[robot]
+    path = yaml_path or os.path.join(_PKG_CONFIG, r["config"])
+    with open(path, "r") as fh:
+        cfg = yaml.safe_load(fh)
+    w = cfg["weights_config"]
+    sites = list(cfg["noncontact_site_list"]) + list(cfg["contact_site_list"])
+    ns = len(sites)
+    assert ns == len(cfg["body_list"]), "autogen.py:42"
+    assert ns == len(r["site_keys"])
+    assert len(cfg["contact_site_list"]) == r["nc"]
+    w_pos = np.array([float(w[f"{k}_translational_tracking"]) for k in r["site_keys"]])
+    w_rot = np.array([float(w[f"{k}_rotational_tracking"]) for k in r["site_keys"]])
+    return OSCModel(name=robot, nv=r["nv"], nu=r["nu"], nc=r["nc"], ns=ns,
+                    mu=float(cfg["friction_coefficient"]), w_pos=w_pos, w_rot=w_rot,
+                    w_torque=float(w["torque"]), w_reg=float(w["regularization"]),
+                    u_lb=np.array(r["u_lb"], float), u_ub=np.array(r["u_ub"], float),
+                    site_dofs=r["site_dofs"])
+
+
+def task_weights(model: OSCModel) -> np.ndarray:
+    """Diagonal of W over the s task rows: [w_p per site x3 ..., w_r per site x3 ...]."""
+    return np.concatenate([np.repeat(model.w_pos, 3), np.repeat(model.w_rot, 3)])
+
+
+def task_targets_vector(model: OSCModel, T: np.ndarray) -> np.ndarray:
+    """t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168 horzsplit/vertsplit)."""
+    T = np.asarray(T, float).reshape(model.ns, 6)
+    return np.concatenate([T[:, 0:3].reshape(-1), T[:, 3:6].reshape(-1)])
+
+
+def contact_jacobian(model: OSCModel, J: np.ndarray) -> np.ndarray:
+    """Jc (nv x 3nc) = rows [3ns-3nc, 3ns) of J, transposed  (osc.h:439-445)."""
+    p = 3 * model.ns
+    return np.asarray(J, float)[p - model.nz:p, :].T.copy()
+
+
+def b_matrix(model: OSCModel) -> np.ndarray:
+    """B = [0_{(nv-nu) x nu}; I_nu]  (go2 autogen.py:53-56, walter autogen.py:53-60)."""
+    B = np.zeros((model.nv, model.nu))
+    B[model.nv - model.nu:, :] = np.eye(model.nu)
+    return B
+
+
+@dataclasses.dataclass
+class QPData:
+    H: np.ndarray
+    f: np.ndarray
+    Aeq: np.ndarray
+    beq: np.ndarray
+    Aineq: np.ndarray
+    bineq: np.ndarray
+    A: np.ndarray
+    l: np.ndarray
+    u: np.ndarray
+
+
+def build_qp(model: OSCModel, M, C, J, b, T, mask) -> QPData:
+    """Closed-form restatement of the six CasADi functions + OSQP stacking for ONE env.
+
+    H = hessian(objective) = blockdiag(2 J^T W J + 2 w_reg I, 2 (w_tau + w_reg) I, 2 w_reg I)
+    f = gradient at x = 0  = [2 J^T W (b - t); 0; 0]
+    Aeq = jacobian(M dv + C - B u - Jc z) = [M, -B, -Jc];   beq = -(C)   (value at x = 0, negated)
+    Aineq = friction pyramid (constant);                   bineq = 0
+    """
+    nv, nu, nz, n = model.nv, model.nu, model.nz, model.n
+    M = np.asarray(M, float).reshape(nv, nv)
+    C = np.asarray(C, float).reshape(nv)
+    J = np.asarray(J, float).reshape(model.s, nv)
+    b = np.asarray(b, float).reshape(model.s)
+    mask = np.asarray(mask, float).reshape(model.nc)
+    Wd = task_weights(model)
+    t = task_targets_vector(model, T)
+
+    H = np.zeros((n, n))
+    H[:nv, :nv] = 2.0 * (J.T * Wd) @ J + 2.0 * model.w_reg * np.eye(nv)
+    H[nv:nv + nu, nv:nv + nu] = 2.0 * (model.w_torque + model.w_reg) * np.eye(nu)
+    H[nv + nu:, nv + nu:] = 2.0 * model.w_reg * np.eye(nz)
+    f = np.zeros(n)
+    f[:nv] = 2.0 * (J.T * Wd) @ (b - t)
+
+    Jc = contact_jacobian(model, J)
+    Aeq = np.hstack([M, -b_matrix(model), -Jc])
+    beq = -C
+
+    mu = model.mu
+    Aineq = np.zeros((4 * model.nc, n))
+    for k in range(model.nc):
+        c0 = nv + nu + 3 * k
+        for r, (sx, sy) in enumerate(((1, 1), (-1, 1), (1, -1), (-1, -1))):   # autogen.py:112-117
+            Aineq[4 * k + r, c0 + 0] = sx
+            Aineq[4 * k + r, c0 + 1] = sy
+            Aineq[4 * k + r, c0 + 2] = -mu
+    bineq = np.zeros(4 * model.nc)
+
+    A = np.vstack([Aeq, Aineq, np.eye(n)])
+    z_lb = np.tile([-OSQP_INFTY, -OSQP_INFTY, 0.0], model.nc)
+    z_ub = np.tile([OSQP_INFTY, OSQP_INFTY, BIG_NUMBER], model.nc)
+    mrep = np.repeat(mask, 3)
+    l = np.concatenate([beq, np.full(4 * model.nc, -OSQP_INFTY), np.full(nv, -OSQP_INFTY),
+                        model.u_lb, z_lb * mrep])
+    u = np.concatenate([beq, bineq, np.full(nv, OSQP_INFTY), model.u_ub, z_ub * mrep])
+    return QPData(H, f, Aeq, beq, Aineq, bineq, A, l, u)
+
+
+def torque(model: OSCModel, x: np.ndarray) -> np.ndarray:
+    """torque_command = solution[nv : nv + nu]  (osc.h:573)."""
+    return np.asarray(x)[model.nv:model.nv + model.nu].copy()

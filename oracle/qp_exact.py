@@ -1,0 +1,187 @@
+"""CPU oracle, part 2: exact solution of the OSC QP + KKT certificate (numpy, fp64).
+
+TEST INFRASTRUCTURE ONLY (see oracle/osc_qp.py header; parity unpinned vs reference outputs).
+
+The reference solves the QP with OSQP 0.6.3 (operational_space_controller.h:346, 507-535) to
+eps_abs = eps_rel = 1e-3 with time-based adaptive rho, so its own torques are only ~1e-3
+accurate and run-to-run non-deterministic.  The QP is strictly convex
+(H >= 2 w_reg I > 0) and always feasible (x = (-M^-1 C, 0, 0)), so its optimum is UNIQUE: that
+optimum is what the product's torques are checked against.
+
+Algorithm here: a textbook primal active-set method (Nocedal & Wright, Alg. 16.3) on the FULL
+reference QP in OSQP form  min 1/2 x'Hx + f'x  s.t.  l <= A x <= u  (equality rows l == u are
+always in the working set), started from a strictly feasible point, finished by an exact KKT
+solve on the final active set.  It shares no code and no algorithm with the product's batched
+interior-point kernel, so agreement between the two is an independent check.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from osc_qp import OSCModel, QPData, b_matrix, contact_jacobian
+
+INF_THRESH = 1e20   # |bound| >= this is "infinite" (the reference uses OSQP_INFTY = 1e30)
+
+
+@dataclasses.dataclass
+class ExactSolution:
+    x: np.ndarray          # primal (n)
+    y: np.ndarray          # OSQP-convention duals (m): H x + f + A' y = 0
+    active: np.ndarray     # bool (m): row at a bound
+    iterations: int
+    cert: dict
+
+
+def _constraints(qp: QPData):
+    """Split l <= Ax <= u into equality rows and one-sided rows (row, sign): sign*a_i x <= sign*bound."""
+    eq, ineq = [], []
+    m, n = qp.A.shape
+    # variables pinned by an identity box row with l == u (masked-off contact forces)
+    pinned = np.zeros(n, bool)
+    for i in range(m - n, m):
+        if qp.l[i] == qp.u[i]:
+            pinned[i - (m - n)] = True
+    for i in range(m):
+        lo, hi = qp.l[i], qp.u[i]
+        if lo == hi:
+            eq.append(i)
+            continue
+        support = np.nonzero(qp.A[i])[0]
+        if i < m - n and pinned[support].all():
+            # row only touches pinned variables (pyramid of a masked contact): it is a
+            # constant 0 <= 0, implied by the pins; keeping it would make the working set
+            # linearly dependent.
+            continue
+        if hi < INF_THRESH:
+            ineq.append((i, +1.0, hi))
+        if lo > -INF_THRESH:
+            ineq.append((i, -1.0, -lo))
+    return eq, ineq
+
+
+def _feasible_start(model: OSCModel, qp: QPData, M, C, J):
+    """Strictly interior point for every one-sided row (u mid-box, z = (0, 0, fz0))."""
+    nv, nu, nz = model.nv, model.nu, model.nz
+    off_u = nv + 4 * model.nc + nv
+    off_z = off_u + nu
+    lu, uu = qp.l[off_u:off_u + nu], qp.u[off_u:off_u + nu]
+    u0 = np.where((lu < 0) & (uu > 0), 0.0, 0.5 * (lu + uu))
+    z0 = np.zeros(nz)
+    for k in range(model.nc):
+        lo, hi = qp.l[off_z + 3 * k + 2], qp.u[off_z + 3 * k + 2]
+        if lo != hi:
+            z0[3 * k + 2] = min(1.0, 0.5 * (lo + hi))
+    rhs = b_matrix(model) @ u0 + contact_jacobian(model, J) @ z0 - np.asarray(C).reshape(-1)
+    dv0 = np.linalg.solve(np.asarray(M).reshape(nv, nv), rhs)
+    return np.concatenate([dv0, u0, z0])
+
+
+def kkt_certificate(qp: QPData, x: np.ndarray, y: np.ndarray) -> dict:
+    """Residuals of the OSQP-form KKT conditions, each scaled to be dimensionless."""
+    Ax = qp.A @ x
+    grad = qp.H @ x + qp.f
+    stat = grad + qp.A.T @ y
+    scale_d = 1.0 + max(np.abs(grad).max(), np.abs(qp.A.T @ y).max())
+    lo_fin = qp.l > -INF_THRESH
+    hi_fin = qp.u < INF_THRESH
+    viol = np.zeros_like(Ax)
+    viol[hi_fin] = np.maximum(viol[hi_fin], Ax[hi_fin] - qp.u[hi_fin])
+    viol[lo_fin] = np.maximum(viol[lo_fin], qp.l[lo_fin] - Ax[lo_fin])
+    bnd = np.where(hi_fin, np.abs(qp.u), 0.0) + np.where(lo_fin, np.abs(qp.l), 0.0)
+    scale_p = 1.0 + max(np.abs(Ax).max(), bnd.max())
+    yp, ym = np.maximum(y, 0.0), np.maximum(-y, 0.0)
+    # dual feasibility: positive y only on finite upper bounds, negative only on finite lower
+    dual_inf = max(np.where(hi_fin, 0.0, yp).max(), np.where(lo_fin, 0.0, ym).max())
+    gap_hi = np.where(hi_fin, qp.u - Ax, 0.0)
+    gap_lo = np.where(lo_fin, Ax - qp.l, 0.0)
+    comp = np.maximum(np.abs(yp * gap_hi), np.abs(ym * gap_lo)).max()
+    return dict(stationarity=float(np.abs(stat).max() / scale_d),
+                primal=float(viol.max() / scale_p),
+                dual=float(dual_inf / scale_d),
+                complementarity=float(comp / (scale_d * scale_p)))
+
+
+def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
+                refine_steps: int = 4) -> ExactSolution:
+    n = model.n
+    eq, ineq = _constraints(qp)
+    A = qp.A
+    x = _feasible_start(model, qp, M, C, J)
+    # sanity: strictly feasible for all one-sided rows
+    for (i, sg, bd) in ineq:
+        assert sg * (A[i] @ x) < bd, "start point not strictly feasible"
+    W: list[int] = []                     # indices into ineq
+    Aeq = A[eq]
+    it = 0
+    for it in range(1, max_iter + 1):
+        # Solve the equality-constrained QP on the working set directly for its minimiser x_W
+        # (more accurate than solving for the step when K is ill-conditioned).
+        rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
+        rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
+        k = rows.shape[0]
+        K = np.zeros((n + k, n + k))
+        K[:n, :n] = qp.H
+        K[:n, n:] = rows.T
+        K[n:, :n] = rows
+        sol = np.linalg.solve(K, np.concatenate([-qp.f, rhs_b]))
+        p, lam = sol[:n] - x, sol[n:]
+        if np.abs(p).max() <= 1e-9 * (1.0 + np.abs(x).max()):
+            x = sol[:n]
+            lam_in = lam[len(eq):]
+            if len(W) == 0 or lam_in.min() >= -1e-10 * (1.0 + np.abs(lam).max()):
+                break
+            W.pop(int(np.argmin(lam_in)))
+            continue
+        alpha, block = 1.0, None
+        for j, (i, sg, bd) in enumerate(ineq):
+            if j in W:
+                continue
+            ap = sg * (A[i] @ p)
+            if ap > 1e-9 * np.abs(p).max():
+                a = (bd - sg * (A[i] @ x)) / ap
+                if a < alpha:
+                    alpha, block = max(a, 0.0), j
+        x = x + alpha * p
+        if block is not None:
+            W.append(block)
+    else:
+        raise RuntimeError("active set did not converge")
+
+    # Final exact KKT solve on the identified active set (removes accumulated step rounding).
+    rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
+    rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
+    k = rows.shape[0]
+    K = np.zeros((n + k, n + k))
+    K[:n, :n] = qp.H
+    K[:n, n:] = rows.T
+    K[n:, :n] = rows
+    rhs = np.concatenate([-qp.f, rhs_b])
+    sol = np.linalg.solve(K, rhs)
+    # Mixed-precision iterative refinement: residuals in x87 extended precision (eps ~1e-19),
+    # corrections from the fp64 factorisation.  Converges to ~eps_ext * cond(K), i.e. well
+    # below fp64 round-off for this QP (cond(K) ~ 1e8..1e10 with w_reg = 1e-4).
+    Kl = K.astype(np.longdouble)
+    rhsl = rhs.astype(np.longdouble)
+    soll = sol.astype(np.longdouble)
+    for _ in range(refine_steps):
+        r = rhsl - Kl @ soll
+        soll = soll + np.linalg.solve(K, r.astype(np.float64)).astype(np.longdouble)
+    sol = soll.astype(np.float64)
+    x, lam = sol[:n], sol[n:]
+    y = np.zeros(A.shape[0])
+    for j, i in enumerate(eq):
+        y[i] += lam[j]
+    active = np.zeros(A.shape[0], bool)
+    active[eq] = True
+    for j, w in enumerate(W):
+        i, sg, _ = ineq[w]
+        y[i] += sg * lam[len(eq) + j]
+        active[i] = True
+    cert = kkt_certificate(qp, x, y)
+    return ExactSolution(x=x, y=y, active=active, iterations=it, cert=cert)
+
+
+def certified(cert: dict, tol: float = 1e-9) -> bool:
+    return all(v <= tol for v in cert.values())

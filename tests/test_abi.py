@@ -1,0 +1,83 @@
+"""CPU tests of the drop-in boundary: libosc_batch.so loads, exports every symbol the header
+declares, parses the reference's YAML schema, and reports errors the documented way.  No
+compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from osc_amd import _lib
+from osc_qp import load_model
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "osc_batch.h")
+REF_CONFIG = "/root/reference/config"
+
+
+def test_library_loads_and_exports_header_symbols():
+    L = _lib.lib()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(osc_\w+)\s*\(", open(HEADER).read(), re.M))
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.osc_abi_version() == 1
+    assert L.osc_status_string(2) == b"OSC_ERR_UNSUPPORTED_DIMS"
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])
+def test_desc_from_yaml_matches_oracle(robot):
+    d = _lib.desc_from_yaml(robot)          # default config next to the library
+    m = load_model(robot)                   # oracle's independent reader (PyYAML)
+    assert (d.nv, d.nu, d.nc, d.ns) == (m.nv, m.nu, m.nc, m.ns)
+    assert d.mu == m.mu and d.w_torque == m.w_torque and d.w_reg == m.w_reg
+    np.testing.assert_array_equal(np.array(d.w_pos[:m.ns]), m.w_pos)
+    np.testing.assert_array_equal(np.array(d.w_rot[:m.ns]), m.w_rot)
+    np.testing.assert_array_equal(np.array(d.u_lb[:m.nu]), m.u_lb)
+    np.testing.assert_array_equal(np.array(d.u_ub[:m.nu]), m.u_ub)
+    assert list(d.z_lb) == [-1e30, -1e30, 0.0] and list(d.z_ub) == [1e30, 1e30, 1e4]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CONFIG), reason="reference tree not mounted")
+@pytest.mark.parametrize("robot,rel", [
+    ("unitree_go2", "unitree_go2/unitree_go2_config.yaml"),
+    ("walter_sr", "walter_sr/walter_sr_config.yaml"),
+    ("walter_sr_wheels", "walter_sr_wheels/walter_sr_wheels_config.yaml"),
+    ("walter_sr", "walter_sr/true_tumbling_mjjoint.yaml"),
+])
+def test_reads_reference_yaml_files(robot, rel):
+    """The native loader reads the reference's own config files (block lists, comments) and
+    agrees with PyYAML on every weight."""
+    path = os.path.join(REF_CONFIG, rel)
+    d = _lib.desc_from_yaml(robot, path)
+    m = load_model(robot, path)
+    np.testing.assert_array_equal(np.array(d.w_pos[:m.ns]), m.w_pos)
+    np.testing.assert_array_equal(np.array(d.w_rot[:m.ns]), m.w_rot)
+    assert d.mu == m.mu
+
+
+def test_error_codes():
+    L = _lib.lib()
+    d = _lib.OscModelDesc()
+    assert L.osc_desc_from_yaml(b"no_such_robot", None, ctypes.byref(d)) == 1
+    assert L.osc_desc_from_yaml(b"unitree_go2", b"/nonexistent.yaml", ctypes.byref(d)) == 3
+    h = ctypes.c_void_p()
+    d = _lib.desc_from_yaml("unitree_go2")
+    d.nv = 17                                   # no compiled kernel for these dimensions
+    assert L.osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 2
+    d = _lib.desc_from_yaml("unitree_go2")
+    d.z_ub[0] = 5.0                             # finite fx bound: not in the reference QP
+    assert L.osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 1
+    assert L.osc_batch_solve(None, 1, *([None] * 10), None) == 1
+    assert L.osc_model_destroy(None) == 1
+
+
+def test_no_device_is_reported_not_faked():
+    """On a host without a HIP device model creation fails loudly (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    h = ctypes.c_void_p()
+    d = _lib.desc_from_yaml("unitree_go2")
+    assert _lib.lib().osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 5

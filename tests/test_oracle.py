@@ -1,0 +1,123 @@
+"""CPU tests of the oracle (oracle/osc_qp.py + oracle/qp_exact.py) against the golden fixtures
+and analytic known-answer cases.  No GPU, no product code on the solve path.
+
+The reference holds no tests or golden vectors: the fixtures are oracle-made and
+parity is unpinned against the reference's own outputs; each case here checks a property the
+reference's QP definition implies (file:line cited per test).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from osc_qp import (BIG_NUMBER, OSQP_INFTY, b_matrix, build_qp, contact_jacobian, load_model,
+                    task_targets_vector, task_weights, torque)
+from qp_exact import certified, kkt_certificate, solve_exact
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+def _load(path):
+    z = np.load(path)          # allow_pickle=False (default): data only
+    return {k: z[k] for k in z.files}
+
+
+def _args(g, e):
+    return [g[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_golden_resolves_and_certifies(path):
+    """Oracle re-solve reproduces every committed golden solution; KKT certificate <= 1e-9."""
+    g = _load(path)
+    model = load_model(str(g["robot"]))
+    for e in range(g["M"].shape[0]):
+        qp = build_qp(model, *_args(g, e))
+        sol = solve_exact(model, qp, *_args(g, e)[:3])
+        assert certified(sol.cert), sol.cert
+        np.testing.assert_allclose(sol.x, g["x"][e], rtol=0, atol=1e-9 * (1 + np.abs(g["x"][e]).max()))
+        np.testing.assert_array_equal(torque(model, g["x"][e]), g["tau"][e])
+        assert certified(kkt_certificate(qp, g["x"][e], g["y"][e]))
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_golden_dynamics_and_bounds(path):
+    """x satisfies M dv + C - B u - Jc z = 0 (autogen.py:87), the friction pyramid
+    (autogen.py:112-117), torque limits (osc.h:285-296) and masked force bounds (osc.h:492-497)."""
+    g = _load(path)
+    model = load_model(str(g["robot"]))
+    nv, nu, nz = model.nv, model.nu, model.nz
+    for e in range(g["M"].shape[0]):
+        x = g["x"][e]
+        dv, u, z = x[:nv], x[nv:nv + nu], x[nv + nu:]
+        Jc = contact_jacobian(model, g["J"][e])
+        res = g["M"][e] @ dv + g["C"][e] - b_matrix(model) @ u - Jc @ z
+        assert np.abs(res).max() <= 1e-9 * (1 + np.abs(g["C"][e]).max())
+        assert np.all(u <= model.u_ub + 1e-9) and np.all(u >= model.u_lb - 1e-9)
+        for k in range(model.nc):
+            fx, fy, fz = z[3 * k:3 * k + 3]
+            if g["mask"][e][k] == 0:
+                assert fx == 0 and fy == 0 and fz == 0          # pinned by l = u = 0
+            else:
+                assert abs(fx) + abs(fy) <= model.mu * fz + 1e-9
+                assert -1e-9 <= fz <= BIG_NUMBER + 1e-9
+
+
+def test_qp_structure_matches_reference():
+    """Closed forms of the CasADi outputs (autogen.py:274-319) and OSQP stacking (osc.h:483-497)."""
+    model = load_model("unitree_go2")
+    g = _load(os.path.join(os.path.dirname(__file__), "golden", "go2_tumbling_mask.npz"))
+    M, C, J, b, T, mask = _args(g, 0)
+    qp = build_qp(model, M, C, J, b, T, mask)
+    nv, nu, nz, n = model.nv, model.nu, model.nz, model.n
+    assert (n, qp.A.shape) == (42, (76, 42))
+    W = task_weights(model)
+    np.testing.assert_allclose(qp.H[:nv, :nv], 2 * J.T @ np.diag(W) @ J + 2e-4 * np.eye(nv))
+    np.testing.assert_array_equal(np.diag(qp.H)[nv:nv + nu], 2 * (1e-4 + 1e-4))
+    np.testing.assert_array_equal(np.diag(qp.H)[nv + nu:], 2 * 1e-4)
+    assert np.count_nonzero(qp.H[:nv, nv:]) == 0
+    np.testing.assert_allclose(qp.f[:nv], 2 * J.T @ (W * (b - task_targets_vector(model, T))))
+    np.testing.assert_array_equal(qp.Aeq[:, :nv], M)
+    np.testing.assert_array_equal(qp.Aeq[:, nv:nv + nu], -b_matrix(model))
+    np.testing.assert_array_equal(qp.Aeq[:, nv + nu:], -J[3 * model.ns - nz:3 * model.ns].T)
+    np.testing.assert_array_equal(qp.beq, -C)
+    np.testing.assert_array_equal(qp.l[:nv], qp.u[:nv])
+    assert np.all(qp.l[nv:nv + 4 * model.nc] == -OSQP_INFTY)
+    np.testing.assert_array_equal(qp.u[nv:nv + 4 * model.nc], 0.0)
+    off = nv + 4 * model.nc + nv
+    np.testing.assert_array_equal(qp.u[off:off + nu], model.u_ub)
+    for k in range(model.nc):
+        lo, hi = qp.l[off + nu + 3 * k:off + nu + 3 * k + 3], qp.u[off + nu + 3 * k:off + nu + 3 * k + 3]
+        if mask[k] == 0:
+            assert np.all(lo == 0) and np.all(hi == 0)
+        else:
+            assert list(lo) == [-OSQP_INFTY, -OSQP_INFTY, 0.0]
+            assert list(hi) == [OSQP_INFTY, OSQP_INFTY, BIG_NUMBER]
+
+
+def test_known_answer_equality_only():
+    """With every contact masked and WaLTER's +-1000 N m limits slack, only the dynamics rows
+    bind: the optimum is the single KKT solve  [H Aeq'; Aeq 0] [x; nu] = [-f; beq]  with z = 0."""
+    g = _load(os.path.join(os.path.dirname(__file__), "golden", "walter_no_contact.npz"))
+    model = load_model("walter_sr")
+    nv, nu, nz, n = model.nv, model.nu, model.nz, model.n
+    for e in range(g["M"].shape[0]):
+        qp = build_qp(model, *_args(g, e))
+        Aeq = np.vstack([qp.Aeq, np.hstack([np.zeros((nz, nv + nu)), np.eye(nz)])])
+        beq = np.concatenate([qp.beq, np.zeros(nz)])
+        k = Aeq.shape[0]
+        K = np.block([[qp.H, Aeq.T], [Aeq, np.zeros((k, k))]])
+        x = np.linalg.solve(K, np.concatenate([-qp.f, beq]))[:n]
+        assert np.all(np.abs(x[nv:nv + nu]) < 1000), "limits must be slack for this check"
+        np.testing.assert_allclose(g["x"][e], x, rtol=0, atol=1e-9 * (1 + np.abs(x).max()))
+
+
+def test_weights_follow_yaml_site_order():
+    """Weight keys map to sites in autogen.py's split order (go2 autogen.py:160-219)."""
+    m = load_model("unitree_go2")
+    np.testing.assert_array_equal(m.w_pos, [100, 10, 10, 10, 10])
+    w = load_model("walter_sr")
+    assert list(w.w_rot[1:5]) == [300.0] * 4 and list(w.w_pos[5:9]) == [100.0] * 4
+    ww = load_model("walter_sr_wheels")
+    assert ww.w_pos[5] == 800.0 and ww.w_rot[0] == 100.0
