@@ -48,6 +48,7 @@
 #ifndef OSC_BATCH_H_
 #define OSC_BATCH_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -116,12 +117,18 @@ int osc_model_destroy(osc_model* model);
 /* Copy of the descriptor a model was created from. */
 int osc_model_get_desc(const osc_model* model, osc_model_desc* desc);
 
-/* Batched solve; see the header comment for layouts.  Device pointers, async on `stream`. */
+/* Device scratch the solve needs for `nenv` environments (the per-env reduced QP handed from
+ * the assembly kernel to the interior-point kernel): 8.5 KB (Go2) / 12.3 KB (WaLTER) per env. */
+int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
+
+/* Batched solve; see the header comment for layouts.  Device pointers, async on `stream`.
+ * `workspace` (16-byte aligned, >= osc_workspace_bytes) may be NULL: the library then takes
+ * stream-ordered scratch (hipMallocAsync / hipFreeAsync) on `stream` for this call. */
 int osc_batch_solve(const osc_model* model, int32_t nenv,
                     const double* M, const double* C, const double* J, const double* b,
                     const double* T, const double* contact_mask,
                     double* tau, double* x, int32_t* status, int32_t* iters,
-                    void* stream);
+                    void* workspace, size_t workspace_bytes, void* stream);
 
 /* Human-readable name of an osc_status. */
 const char* osc_status_string(int status);

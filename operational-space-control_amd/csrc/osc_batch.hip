@@ -1,4 +1,4 @@
-// osc_batch.hip -- batched OSC QP assembly + solve for gfx950 (MI355X), one wavefront per env.
+// osc_batch.hip -- batched OSC QP assembly + solve for gfx950 (MI355X).
 //
 // Replaces, per environment, the reference's per-tick hot path (paths relative to the
 // reference's operational-space-control/ directory):
@@ -12,39 +12,44 @@
 //   s.t.   M dv + C - B u - Jc z = 0            B = [0; I_nu],  Jc = Jp[last 3nc rows]^T
 //          (+-fx +-fy - mu fz) <= 0 per contact, fz in [z_lb, z_ub] * mask, u in [u_lb, u_ub]
 //
-// Method (see DESIGN.md §3 for the derivation and the accuracy study):
+// Method:
 //   1. u is eliminated exactly from the actuated dynamics rows, and the base accelerations
-//      dv_b from the 6 unactuated rows through the 6x6 base block M_bb only:
+//      dv_b from the unactuated rows through the base block M_bb only:
 //         dv_b = M_bb^-1 (-M_ba dv_a + Jc_b z - C_b),   u = M_a dv + C_a - Jc_a z.
-//      The remaining variables y = (dv_a, z) (nu + 3nc = 24 Go2 / 32 WaLTER) carry a dense
-//      reduced Hessian Hr and gradient g.  Inverting only M_bb (never the full M) keeps the
-//      regularisation-only curvature (2 w_reg = 2e-4, internal contact forces) resolvable in
-//      fp64: torque error vs the exact optimum drops ~10x against the full-M^-1 reduction.
+//      The unknowns y = (dv_a, z) (24 Go2 / 32 WaLTER) carry a dense reduced Hessian Hr and
+//      gradient g.  Inverting only M_bb keeps the regularisation-only curvature
+//      (2 w_reg = 2e-4: internal contact forces) resolvable in fp64.
 //   2. Mehrotra predictor-corrector interior point on  min 1/2 y'Hr y + g'y  s.t. G y <= h,
-//      with G = [+-U (torque bounds, dense rows); pyramid + fz bound rows (sparse)].
-//      Newton matrix K = Hr + G' diag(lambda/s) G factorised by LDL^T with "Cholesky-infinity"
-//      pivots (a pivot below 1e-13 of its original diagonal is replaced by 1e128).
+//      G = [+-U (torque bounds, dense rows); pyramid + fz bound rows (sparse)].  Newton matrix
+//      K = Hr + G' diag(lambda/s) G, LDL^T with "Cholesky-infinity" pivots.
 //
-// Mapping onto CDNA4: one 64-lane wavefront = one environment = one workgroup.  Inputs are
-// staged HBM -> LDS with 16-byte loads.  Dense products (J'WJ, the reduced Hessian) give every
-// lane several output entries.  The Newton matrix lives in REGISTERS, one column per lane
-// (lane j holds K[:, j]); the right-looking LDL^T broadcasts pivot column k with
-// v_readlane, and both triangular solves run on lane-local data plus one broadcast per step
-// (the symmetric trailing-matrix trick keeps row j of L in lane j's upper registers).
-// Inequality rows map one per lane (48 Go2 / 64 WaLTER), so all interior-point vector work
-// (residuals, ratio tests, complementarity) is lane-parallel with wavefront reductions.
+// Two kernels, one workspace (per env [Hr | g | U | X], fp64):
+//   osc_setup_kernel  one 64-lane wavefront per environment.  Inputs are staged HBM -> LDS
+//                     with 16-byte loads; the dense products (J'WJ, the reduced Hessian) give
+//                     every lane several output entries.
+//   osc_ipm_kernel    FOUR environments per wavefront, one 16-lane DPP row each.  The Newton
+//                     matrix lives in registers, lane l holding columns l and l+16.  The
+//                     right-looking LDL^T broadcasts the pivot column inside each row with
+//                     v_mov_b64_dpp row_newbcast -- a VALU operation, no LDS traffic -- and the
+//                     triangular solves use lane-local data (the symmetric trailing update
+//                     leaves row j of L in lane j's upper registers) plus one row broadcast per
+//                     step.  Inequality rows map three/four per lane; reductions (ratio test,
+//                     complementarity) are 16-lane DPP butterflies.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <new>
+#include <type_traits>
 
 #include "osc_batch.h"
 
 namespace {
 
 constexpr int kWave = 64;
+constexpr int kRow = 16;                 // lanes per environment in the IPM kernel (DPP row)
+constexpr int kEnvPerWave = kWave / kRow;
 
 // Per-model constants, device-resident (uniform loads -> scalar cache).
 struct DevParams {
@@ -62,7 +67,7 @@ struct DevParams {
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS regions 16-byte aligned
+constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regions 16-B aligned
 
 template <int NV_, int NU_, int NC_, int NS_>
 struct Dims {
@@ -71,36 +76,57 @@ struct Dims {
   static constexpr int NZ = 3 * NC;
   static constexpr int NY = NU + NZ;          // reduced variables (dv_a, z)
   static constexpr int NY1 = NY + 1;          // + affine column
+  static constexpr int NY1P = even(NY1);      // padded row stride of U and X
   static constexpr int S = 6 * NS;            // task rows
   static constexpr int MI = 2 * NU + 6 * NC;  // inequality rows (u box, pyramid, fz box)
   static constexpr int NX = NV + NU + NZ;     // design vector
   static constexpr int NA = NV + 1;           // [J | e] Gram size
   static constexpr int NPA = NA * (NA + 1) / 2;
   static constexpr int NPH = NY1 * (NY1 + 1) / 2 - 1;   // reduced Hessian pairs (no corner)
-  static_assert(NY1 <= kWave && MI <= kWave && NX <= kWave, "one row/column per lane");
+  static constexpr int NRL = (MI + kRow - 1) / kRow;    // inequality rows per lane (IPM)
+  static_assert(NY1 <= kWave && NX <= 3 * kRow, "setup / output lane mapping");
+  static_assert(NY > kRow && NY <= 2 * kRow, "IPM: two column slots per lane");
+  static_assert(NU <= kRow && NB <= kRow, "IPM: one torque / base row per lane");
   static_assert(NB >= 1 && NB <= 8, "floating-base block");
 
-  // ---- LDS layout (doubles).  R1/R2 are reused between phases. ----
+  // ---- workspace per env (doubles): [g | U | Hr | X] ----
+  static constexpr int W_G = 0;
+  static constexpr int W_U = even(NY);
+  static constexpr int W_HR = W_U + NU * NY1P;
+  static constexpr int W_X = W_HR + even(NY * NY);
+  static constexpr int WS = W_X + NB * NY1P;
+
+  // ---- setup-kernel LDS (doubles).  R1/R2 are reused between phases. ----
   static constexpr int R1_A = even(S * NV) + even(S) + even(NS * 6);   // J | e | T
   static constexpr int R1_D = even(NV * NY1) + even(NY * NY);           // T1 | Hr
   static constexpr int R1 = cmax(R1_A, R1_D);
-  static constexpr int R2_A = even(NV * NV) + even(NV);                 // M | C
-  static constexpr int R2_E = 4 * even(NY) + 3 * kWave + even(NU);      // IPM vectors
-  static constexpr int R2 = cmax(R2_A, R2_E);
+  static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
   static constexpr int O_J = 0, O_E = even(S * NV), O_T = O_E + even(S);
   static constexpr int O_T1 = 0, O_HR = even(NV * NY1);
-  static constexpr int O_R2 = R1;
-  static constexpr int O_M = O_R2, O_C = O_R2 + even(NV * NV);
-  static constexpr int O_VY = O_R2, O_VY2 = O_VY + even(NY), O_DG = O_VY2 + even(NY),
-                       O_G = O_DG + even(NY), O_VR = O_G + even(NY), O_DR = O_VR + kWave,
-                       O_VR2 = O_DR + kWave, O_TAU = O_VR2 + kWave;   // row vectors: one per lane
-  static constexpr int O_HA = O_R2 + R2;
+  static constexpr int O_M = R1, O_C = R1 + even(NV * NV), O_G = R1;
+  static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
-  static constexpr int O_U = O_X + even(NB * NY1);
-  static constexpr int O_MASK = O_U + even(NU * NY1);
+  static constexpr int O_U = O_X + NB * NY1P;
+  static constexpr int O_MASK = O_U + NU * NY1P;
   static constexpr int SMEM = O_MASK + even(NC);
-  static constexpr int DBG = NY * NY + NY + NU * NY1 + NB * NY1;   // debug dump per env
-  static_assert(SMEM * 8 <= 64 * 1024, "LDS budget per env");
+  static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
+
+  // ---- IPM-kernel LDS per env (doubles): workspace prefix [g | U] + vectors.  Hr is NOT in
+  // LDS: each lane streams its two Hr columns from the (L2-resident) workspace straight into
+  // the Newton-matrix registers once per iteration, which keeps the LDS footprint small
+  // enough for two waves per SIMD. ----
+  static constexpr int I_G = W_G, I_U = W_U;
+  static constexpr int I_VY = W_HR;                    // y (current iterate)
+  static constexpr int I_VY2 = I_VY + even(NY);        // search direction
+  static constexpr int I_UV = I_VY2 + even(NY);        // U_y v for the torque rows
+  static constexpr int I_VR = I_UV + even(NU);         // a row-space vector
+  static constexpr int I_DR = I_VR + NRL * kRow;       // lambda / s
+  static constexpr int I_DINV = I_DR + NRL * kRow;     // 1 / D of the LDL^T factor
+  static constexpr int I_DG = I_DINV + even(NY);       // original diagonal of K
+  static constexpr int I_MASK = I_DG + even(NY);
+  static constexpr int I_TAU = I_MASK + even(NC);
+  static constexpr int I_XB = I_TAU + even(NU);
+  static constexpr int IL = I_XB + even(NB);
 };
 
 // Upper-triangle pair tables (i <= j), built at compile time.
@@ -124,7 +150,15 @@ struct Pairs {
 template <int N, bool SKIP>
 __device__ constexpr Pairs<N, SKIP> kPairs{};
 
-// ---- wavefront primitives -------------------------------------------------------------------
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// ---- lane primitives ----------------------------------------------------------------------
 // An empty asm that "modifies" x: comparisons against the lane id made right after it cannot
 // be hoisted out of loops (hipcc otherwise precomputes one 64-bit lane mask per unrolled step,
 // hundreds of SGPRs, and spills them).
@@ -133,112 +167,112 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
-__device__ __forceinline__ double bcast(double v, int k) {
-  int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
-  int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
-  return __hiloint2double(hi, lo);
+// Broadcast lane K of each 16-lane row to the whole row: v_mov_b64_dpp row_newbcast:K.
+template <int K>
+__device__ __forceinline__ double rowb(double v) {
+  const long long x = __double_as_longlong(v);
+  return __longlong_as_double(__builtin_amdgcn_mov_dpp(x, 0x150 + K, 0xf, 0xf, false));
 }
 
-// xor-butterfly inside each 32-lane half with ds_swizzle (bitmask mode), halves combined with
-// two readlanes: the result is wave-uniform and bitwise identical on every lane.
-template <int XOR>
-__device__ __forceinline__ double swz_xor(double v) {
-  constexpr int pat = (XOR << 10) | 0x1f;
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+template <int CTRL>
+__device__ __forceinline__ double dpp32x2(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double wave_sum(double v) {
-  v += swz_xor<1>(v);
-  v += swz_xor<2>(v);
-  v += swz_xor<4>(v);
-  v += swz_xor<8>(v);
-  v += swz_xor<16>(v);
-  return bcast(v, 0) + bcast(v, 32);
+// 16-lane row reductions: quad_perm xor1 / xor2, row_half_mirror, row_mirror.  Every lane of
+// the row ends with the bitwise-identical result (each combine is commutative).
+__device__ __forceinline__ double row_sum(double v) {
+  v += dpp32x2<0xB1>(v);
+  v += dpp32x2<0x4E>(v);
+  v += dpp32x2<0x141>(v);
+  v += dpp32x2<0x140>(v);
+  return v;
 }
-__device__ __forceinline__ double wave_min(double v) {
-  v = fmin(v, swz_xor<1>(v));
-  v = fmin(v, swz_xor<2>(v));
-  v = fmin(v, swz_xor<4>(v));
-  v = fmin(v, swz_xor<8>(v));
-  v = fmin(v, swz_xor<16>(v));
-  return fmin(bcast(v, 0), bcast(v, 32));
+__device__ __forceinline__ double row_min(double v) {
+  v = fmin(v, dpp32x2<0xB1>(v));
+  v = fmin(v, dpp32x2<0x4E>(v));
+  v = fmin(v, dpp32x2<0x141>(v));
+  v = fmin(v, dpp32x2<0x140>(v));
+  return v;
 }
-__device__ __forceinline__ double wave_max(double v) {
-  v = fmax(v, swz_xor<1>(v));
-  v = fmax(v, swz_xor<2>(v));
-  v = fmax(v, swz_xor<4>(v));
-  v = fmax(v, swz_xor<8>(v));
-  v = fmax(v, swz_xor<16>(v));
-  return fmax(bcast(v, 0), bcast(v, 32));
+__device__ __forceinline__ double row_max(double v) {
+  v = fmax(v, dpp32x2<0xB1>(v));
+  v = fmax(v, dpp32x2<0x4E>(v));
+  v = fmax(v, dpp32x2<0x141>(v));
+  v = fmax(v, dpp32x2<0x140>(v));
+  return v;
+}
+
+// ---- diagnostic stamps (OSC_STAMPS builds only; the product build compiles them out) ----
+// Per wave, cycles (s_memtime) accumulated per IPM phase; read back by osc_debug_stamps.
+#ifdef OSC_STAMPS
+constexpr int kStampSlots = 8;
+constexpr int kStampBlocks = 1 << 15;
+__device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
+#define STAMP_DECL unsigned long long st_acc[kStampSlots] = {}; unsigned long long st_t0 = 0;
+#define STAMP_BEGIN()                                                        \
+  do {                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t0)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+  } while (0)
+#define STAMP_END(slot)                                                      \
+  do {                                                                       \
+    unsigned long long st_t1;                                                \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t1)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    st_acc[slot] += st_t1 - st_t0;                                           \
+  } while (0)
+#define STAMP_STORE()                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                       \
+      for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
+        g_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];                \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END(slot) do {} while (0)
+#define STAMP_STORE() do {} while (0)
+#endif
+
+// Both kernels run ONE wavefront per workgroup.  LDS instructions of a wavefront execute in
+// program order, so ordering an LDS write before another lane's later read only needs the
+// compiler not to move memory operations across this point.  Unlike __syncthreads() (whose
+// workgroup release fence emits s_waitcnt vmcnt(0)), it leaves in-flight global loads alone:
+// the Hr prefetch of the IPM kernel stays in flight across it.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 1/d to full double precision: v_rcp_f64 + two Newton steps.
+__device__ __forceinline__ double recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
 }
 
 // Copy n doubles (n even, both pointers 16-byte aligned) global -> LDS, 16 B per lane.
-__device__ __forceinline__ void stage(double* dst, const double* __restrict__ src, int n, int lane) {
+__device__ __forceinline__ void stage(double* dst, const double* __restrict__ src, int n, int lane,
+                                      int stride = kWave) {
   const double2* s2 = reinterpret_cast<const double2*>(src);
   double2* d2 = reinterpret_cast<double2*>(dst);
-  for (int i = lane; i < n / 2; i += kWave) d2[i] = s2[i];
+  for (int i = lane; i < n / 2; i += stride) d2[i] = s2[i];
 }
 
-// ---- register-resident LDL^T, one column per lane ------------------------------------------
-// On entry lane j < N holds c[i] = K[i][j] (K symmetric).  On exit:
-//   c[i], i > j : L[i][j]            (unit lower factor, column j)
-//   c[i], i < j : L[j][i] * D[i]     (row j of L, scaled -- left by the symmetric update)
-//   dinv        : 1 / D[j]
-// `sdg` (LDS) holds the original diagonal (for the Cholesky-infinity test); `sdinv` (LDS)
-// receives 1/D for the solves.
-template <int N>
-__device__ __forceinline__ void ldl_columns(double (&c)[N], double& dinv, const double* sdg,
-                                            double* sdinv, int lane) {
-  dinv = 0.0;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    double dk = bcast(c[k], k);
-    const double dg = sdg[k];
-    if (!(dk > 1e-13 * dg)) dk = 1e128;   // Cholesky-infinity (Wright; PCx)
-    const double inv = 1.0 / dk;
-    const int ln = opaque(lane);
-    if (ln == k) dinv = inv;
-    const double t = (ln > k && ln < N) ? c[k] * inv : 0.0;   // L[lane][k]
-#pragma unroll
-    for (int i = k + 1; i < N; ++i) c[i] = fma(-bcast(c[i], k), t, c[i]);
-  }
-  // scale the column part (i > lane) into unit-lower L
-#pragma unroll
-  for (int i = 0; i < N; ++i) c[i] = (i > opaque(lane)) ? c[i] * dinv : c[i];
-  if (lane < N) sdinv[lane] = dinv;
-  __syncthreads();
-}
-
-// Solve K x = r with the factor above.  Lane j holds r_j on entry, x_j on exit.
-template <int N>
-__device__ __forceinline__ double ldl_solve(const double (&c)[N], double dinv, const double* sdinv,
-                                            double r, int lane) {
-  double acc = r;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {          // forward: L z = r
-    const double zs = bcast(acc, k) * sdinv[k];
-    acc = (opaque(lane) > k) ? fma(-c[k], zs, acc) : acc;
-  }
-  acc *= dinv;                           // D w = z
-#pragma unroll
-  for (int k = N - 1; k >= 0; --k) {     // backward: L^T x = w
-    const double xk = bcast(acc, k);
-    acc = (opaque(lane) < k) ? fma(-c[k], xk, acc) : acc;
-  }
-  return acc;
-}
-
-// ---- the kernel ----------------------------------------------------------------------------
+// ============================ kernel 1: reduced QP per env ==================================
 template <class D>
-__global__ __launch_bounds__(kWave) void osc_solve_kernel(
+__global__ __launch_bounds__(kWave) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
-    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ gtau,
-    double* __restrict__ gx, int32_t* __restrict__ gstatus, int32_t* __restrict__ giters,
-    double* __restrict__ gdbg) {
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
-                NY1 = D::NY1, S = D::S, MI = D::MI, NA = D::NA;
+                NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NA = D::NA;
   __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
@@ -255,6 +289,7 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
   double* sMask = sm + D::O_MASK;
   double* sT1 = sm + D::O_T1;
   double* sHr = sm + D::O_HR;
+  double* sG = sm + D::O_G;
 
   // ---------------- Phase A: stage this env's inputs HBM -> LDS ----------------
   stage(sJ, gJ + static_cast<size_t>(env) * S * NV, S * NV, lane);
@@ -263,13 +298,13 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
   stage(sE, gb + static_cast<size_t>(env) * S, S, lane);
   stage(sT, gT + static_cast<size_t>(env) * NS * 6, NS * 6, lane);
   stage(sMask, gmask + static_cast<size_t>(env) * NC, NC, lane);
-  __syncthreads();
+  wave_sync();
   // e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]   (autogen.py:163-168)
   for (int r = lane; r < S; r += kWave) {
     const int half = r / (3 * NS), rr = r % (3 * NS);
     sE[r] -= sT[(rr / 3) * 6 + half * 3 + rr % 3];
   }
-  __syncthreads();
+  wave_sync();
 
   // ---------------- Phase B: Ha = 2 [J e]' W [J e]  (H_dv block and f_dv column) -------------
   // H_dv = 2 J'WJ + 2 w_reg I,  f_dv = 2 J'W (b - t)   (autogen.py:131-238, 304-319)
@@ -288,7 +323,7 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
   }
 
   // ---------------- Phase C: base-block elimination  X = M_bb^-1 [-M_ba | Jc_b | -C_b] -------
-  // and the torque map U = M_a P + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
+  // and the torque map U = M_a Pm + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
   // (dynamics rows: autogen.py:58-89; Jc = Jp[last 3nc rows]^T: osc.h:439-445)
   constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
   if (lane < NY1) {
@@ -333,7 +368,7 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
 #pragma unroll
       for (int i = 0; i < k; ++i) x[i] = fma(-L[k][i], x[k], x[i]);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) sX[i * NY1 + c] = x[i];
+    for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = x[i];
     for (int a = 0; a < NU; ++a) {
       double acc;
       if (c < NU) acc = sM[(NB + a) * NV + NB + c];
@@ -342,10 +377,10 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
       if (pinned) acc = 0.0;
 #pragma unroll
       for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
-      sU[a * NY1 + c] = acc;
+      sU[a * NY1P + c] = acc;
     }
   }
-  __syncthreads();   // J, M, C dead from here on (R1, R2 get reused)
+  wave_sync();   // J, M, C dead from here on (R1, R2 get reused)
 
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
   // dv = Pm [y;1] with Pm = [X ; (I_nu 0 0)],  T1 = H_dv Pm (+ f_dv in the affine column),
@@ -354,11 +389,10 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
     const int r = idx / NY1, c = idx % NY1;
     double acc = (c < NU) ? sHa[r * NA + NB + c] : ((c == NY) ? sHa[r * NA + NV] : 0.0);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) acc = fma(sHa[r * NA + i], sX[i * NY1 + c], acc);
+    for (int i = 0; i < NB; ++i) acc = fma(sHa[r * NA + i], sX[i * NY1P + c], acc);
     sT1[r * NY1 + c] = acc;
   }
-  __syncthreads();
-  double* sG = sm + D::O_G;
+  wave_sync();
   {
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
@@ -366,10 +400,10 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
       const int a = kPairs<NY1, true>.a[p], b = kPairs<NY1, true>.b[p];
       double acc = (a < NU) ? sT1[(NB + a) * NY1 + b] : 0.0;
 #pragma unroll
-      for (int r = 0; r < NB; ++r) acc = fma(sX[r * NY1 + a], sT1[r * NY1 + b], acc);
+      for (int r = 0; r < NB; ++r) acc = fma(sX[r * NY1P + a], sT1[r * NY1 + b], acc);
       double uu = 0.0;
 #pragma unroll
-      for (int q = 0; q < NU; ++q) uu = fma(sU[q * NY1 + a], sU[q * NY1 + b], uu);
+      for (int q = 0; q < NU; ++q) uu = fma(sU[q * NY1P + a], sU[q * NY1P + b], uu);
       acc = fma(wu2, uu, acc);
       if (b < NY) {
         if (a == b && a >= NU) {
@@ -383,83 +417,191 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
       }
     }
   }
-  __syncthreads();
+  wave_sync();
 
-  if (gdbg != nullptr) {   // test hook (osc_debug_reduced_qp): dump the reduced QP
-    double* o = gdbg + static_cast<size_t>(env) * D::DBG;
-    for (int i = lane; i < NY * NY; i += kWave) o[i] = sHr[i];
-    for (int i = lane; i < NY; i += kWave) o[NY * NY + i] = sG[i];
-    for (int i = lane; i < NU * NY1; i += kWave) o[NY * NY + NY + i] = sU[i];
-    for (int i = lane; i < NB * NY1; i += kWave) o[NY * NY + NY + NU * NY1 + i] = sX[i];
+  // ---------------- write the reduced QP: workspace [Hr | g | U | X] -------------------------
+  double* w = ws + static_cast<size_t>(env) * D::WS;
+  for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
+  for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
+  for (int i = lane; i < NU * NY1P; i += kWave) w[D::W_U + i] = sU[i];
+  for (int i = lane; i < NB * NY1P; i += kWave) w[D::W_X + i] = sX[i];
+}
+
+// ============================ kernel 2: interior point, 4 env / wave ========================
+
+// LDL^T of an N x N symmetric matrix held one column per lane in two slots: lane l of a row
+// holds column l in c0 and column l+16 in c1.  On exit (for slot column j):
+//   c[i], i > j : L[i][j]            (unit lower factor, column j)
+//   c[i], i < j : L[j][i] * D[i]     (row j of L, scaled -- left by the symmetric update)
+//   dinv        : 1 / D[j]
+// sdg: original diagonal (Cholesky-infinity test); sdinv receives 1/D for the solves.
+template <int N>
+__device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double& dinv0,
+                                         double& dinv1, const double* sdg, double* sdinv,
+                                         int l) {
+  dinv0 = 0.0;
+  dinv1 = 0.0;
+  static_for<0, N>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    double dk = (s == 0) ? rowb<kl>(c0[k]) : rowb<kl>(c1[k]);
+    if (!(dk > 1e-13 * sdg[k])) dk = 1e128;   // Cholesky-infinity (Wright; PCx)
+    const double inv = recip(dk);
+    const int ln = opaque(l);
+    if constexpr (s == 0) {
+      dinv0 = (ln == kl) ? inv : dinv0;
+    } else {
+      dinv1 = (ln == kl) ? inv : dinv1;
+    }
+    const double t0 = (k < kRow - 1 && ln > k) ? -c0[k] * inv : 0.0;   // -L[lane][k]
+    const double t1 = (ln + kRow > k && ln + kRow < N) ? -c1[k] * inv : 0.0;
+    static_for<k + 1, N>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const double b = (s == 0) ? rowb<kl>(c0[i]) : rowb<kl>(c1[i]);
+      c1[i] = fma(b, t1, c1[i]);
+      if constexpr (k < kRow - 1) c0[i] = fma(b, t0, c0[i]);
+    });
+  });
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int ln = opaque(l);
+    c0[i] = (i > ln) ? c0[i] * dinv0 : c0[i];
+    c1[i] = (i > ln + kRow) ? c1[i] * dinv1 : c1[i];
   }
+  sdinv[l] = dinv0;
+  if (l + kRow < N) sdinv[l + kRow] = dinv1;
+}
 
-  // ---------------- Phase E: Mehrotra predictor-corrector interior point ------------------
-  double* sVy = sm + D::O_VY;     // broadcast copy of a y-space vector
-  double* sVy2 = sm + D::O_VY2;
-  double* sDg = sm + D::O_DG;     // original diagonal of K
-  double* sVr = sm + D::O_VR;     // broadcast copy of a row-space vector
-  double* sDr = sm + D::O_DR;     // lambda / s
-  double* sDinv = sm + D::O_VR2;  // 1 / D of the LDL^T factor (NY <= MI entries)
-  double* sTau = sm + D::O_TAU;
+// Solve K x = r with the factor above; slot values r0 (var l), r1 (var l+16) in, x out.
+template <int N>
+__device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const double (&c1)[N],
+                                               double dinv0, double dinv1, const double* sdinv,
+                                               double& a0, double& a1, int l) {
+  static_for<0, N>([&](auto kc) {           // forward: L z = r
+    constexpr int k = decltype(kc)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    const double zs = ((s == 0) ? rowb<kl>(a0) : rowb<kl>(a1)) * sdinv[k];
+    const int ln = opaque(l);
+    if constexpr (k < kRow - 1) a0 = (ln > k) ? fma(-c0[k], zs, a0) : a0;
+    a1 = (ln + kRow > k) ? fma(-c1[k], zs, a1) : a1;
+  });
+  a0 *= dinv0;                              // D w = z
+  a1 *= dinv1;
+  static_for<0, N>([&](auto kc) {           // backward: L^T x = w
+    constexpr int k = N - 1 - decltype(kc)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    const double xk = (s == 0) ? rowb<kl>(a0) : rowb<kl>(a1);
+    const int ln = opaque(l);
+    if constexpr (k >= 1) a0 = (ln < k) ? fma(-c0[k], xk, a0) : a0;
+    if constexpr (k > kRow) a1 = (ln + kRow < k) ? fma(-c1[k], xk, a1) : a1;
+  });
+}
 
-  // Row description for this lane (row r = lane).
-  const int r = lane;
-  bool act = false;
-  double h = 0.0;
-  int rq = 0, rk = 0, rt = 0;        // u-row index / contact / row type
-  double rsg = 0.0;
-  if (r < 2 * NU) {
-    rq = r >> 1;
-    rsg = (r & 1) ? -1.0 : 1.0;
-    const double bnd = (r & 1) ? P->u_lb[rq] : P->u_ub[rq];
-    act = fabs(bnd) < P->inf_thresh;
-    h = rsg * (bnd - sU[rq * NY1 + NY]);
-  } else if (r < MI) {
-    rk = (r - 2 * NU) / 6;
-    rt = (r - 2 * NU) % 6;
-    const double m = sMask[rk];
-    if (m != 0.0) {
-      if (rt < 4) {
-        act = true;                                   // friction pyramid, bineq = 0
-        h = 0.0;
-      } else if (rt == 4) {
-        const double lb = P->z_lb[2] * m;             // -fz <= -lb
-        act = fabs(lb) < P->inf_thresh;
-        h = -lb;
-      } else {
-        const double ub = P->z_ub[2] * m;             // fz <= ub
-        act = fabs(ub) < P->inf_thresh;
-        h = ub;
+template <class D>
+__global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
+    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters) {
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
+                MI = D::MI, NRL = D::NRL;
+  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * D::IL];
+  const int lane = threadIdx.x;
+  const int grp = lane / kRow, l = lane % kRow;
+  const int env_raw = blockIdx.x * kEnvPerWave + grp;
+  const bool valid = env_raw < nenv;
+  const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
+
+  double* B = sm + grp * D::IL;
+  const double* gHr = ws + static_cast<size_t>(env) * D::WS + D::W_HR;   // global, L2-resident
+  double* sG = B + D::I_G;
+  double* sU = B + D::I_U;
+  double* sVy = B + D::I_VY;
+  double* sVy2 = B + D::I_VY2;
+  double* sUv = B + D::I_UV;
+  double* sVr = B + D::I_VR;
+  double* sDr = B + D::I_DR;
+  double* sDinv = B + D::I_DINV;
+  double* sDg = B + D::I_DG;
+  double* sMask = B + D::I_MASK;
+  double* sTau = B + D::I_TAU;
+  double* sXb = B + D::I_XB;
+
+  STAMP_DECL
+  STAMP_BEGIN();
+  // stage [g | U] (the workspace prefix has the LDS layout) and the mask
+  stage(B, ws + static_cast<size_t>(env) * D::WS, D::W_HR, l, kRow);
+  for (int i = l; i < NC; i += kRow) sMask[i] = gmask[static_cast<size_t>(env) * NC + i];
+  wave_sync();
+
+  // ---- inequality rows of this lane: r = l + 16 t.  Only (active, h) are kept; the row's
+  // kind (torque bound q / sign, or contact k / pyramid side) is recomputed from r. ----
+  bool act[NRL];
+  double h[NRL];
+#pragma unroll
+  for (int t = 0; t < NRL; ++t) {
+    const int r = l + kRow * t;
+    act[t] = false;
+    h[t] = 0.0;
+    if (r < 2 * NU) {
+      const int q = r >> 1;
+      const double sg = (r & 1) ? -1.0 : 1.0;
+      const double bnd = (r & 1) ? P->u_lb[q] : P->u_ub[q];
+      act[t] = fabs(bnd) < P->inf_thresh;
+      h[t] = sg * (bnd - sU[q * NY1P + NY]);
+    } else if (r < MI) {
+      const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
+      const double m = sMask[k];
+      if (m != 0.0) {
+        if (rt < 4) {
+          act[t] = true;                                   // friction pyramid, bineq = 0
+        } else if (rt == 4) {
+          const double lb = P->z_lb[2] * m;                // -fz <= -lb
+          act[t] = fabs(lb) < P->inf_thresh;
+          h[t] = -lb;
+        } else {
+          const double ub = P->z_ub[2] * m;                // fz <= ub
+          act[t] = fabs(ub) < P->inf_thresh;
+          h[t] = ub;
+        }
       }
     }
   }
   const double mu_f = P->mu;
-  const double psx = (rt & 1) ? -1.0 : 1.0;   // pyramid row signs: (1,1),(-1,1),(1,-1),(-1,-1)
-  const double psy = (rt >= 2) ? -1.0 : 1.0;
-  const int zc0 = NU + 3 * rk;
+  STAMP_END(0);
 
-  // (G v)_r for v staged in LDS
-  auto Gv = [&](const double* v) -> double {
-    double acc = 0.0;
-    if (!act) return 0.0;
-    if (r < 2 * NU) {
+  // U_y v for the torque rows (lanes l < NU), result in sUv; caller syncs
+  auto uv_product = [&](const double* v) {
+    if (l < NU) {
+      double a = 0.0;
 #pragma unroll
-      for (int i = 0; i < NY; ++i) acc = fma(sU[rq * NY1 + i], v[i], acc);
-      return rsg * acc;
+      for (int i = 0; i < NY; ++i) a = fma(sU[l * NY1P + i], v[i], a);
+      sUv[l] = a;
     }
-    if (rt < 4) return psx * v[zc0] + psy * v[zc0 + 1] - mu_f * v[zc0 + 2];
-    return (rt == 4) ? -v[zc0 + 2] : v[zc0 + 2];
   };
-  // Column role for lane j (var j)
-  const int j = lane;
-  const int jk = (j >= NU && j < NY) ? (j - NU) / 3 : -1;
-  const int jc = (j >= NU && j < NY) ? (j - NU) % 3 : 0;
-  // (G' w)_j for w staged in LDS (inactive rows hold 0)
-  auto GTw = [&](const double* w) -> double {
+  // (G v)_r for row slot t, given sUv = U_y v
+  auto Gv = [&](const double* v, int t) -> double {
+    if (!act[t]) return 0.0;
+    const int r = l + kRow * t;
+    if (r < 2 * NU) return (r & 1) ? -sUv[r >> 1] : sUv[r >> 1];
+    const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
+    const int z0 = NU + 3 * k;
+    if (rt < 4) {
+      const double sx = (rt & 1) ? -1.0 : 1.0, sy = (rt >= 2) ? -1.0 : 1.0;
+      return sx * v[z0] + sy * v[z0 + 1] - mu_f * v[z0 + 2];
+    }
+    return (rt == 4) ? -v[z0 + 2] : v[z0 + 2];
+  };
+  // variable slots of this lane: j = l + 16 s
+  const int j0 = l, j1 = l + kRow;
+  const bool v1 = j1 < NY;
+  const int jj1 = v1 ? j1 : NY - 1;
+  const int jk0 = (j0 >= NU) ? (j0 - NU) / 3 : -1, jc0 = (j0 >= NU) ? (j0 - NU) % 3 : 0;
+  const int jk1 = (v1 && j1 >= NU) ? (j1 - NU) / 3 : -1, jc1 = (j1 >= NU) ? (j1 - NU) % 3 : 0;
+  // (G' w)_j for row-space w staged in LDS (inactive rows hold 0)
+  auto GTw = [&](const double* w, int jj, int jk, int jc) -> double {
     double acc = 0.0;
-    if (j >= NY) return 0.0;
 #pragma unroll
-    for (int q = 0; q < NU; ++q) acc = fma(sU[q * NY1 + j], w[2 * q] - w[2 * q + 1], acc);
+    for (int q = 0; q < NU; ++q) acc = fma(sU[q * NY1P + jj], w[2 * q] - w[2 * q + 1], acc);
     if (jk >= 0) {
       const double* wk = w + 2 * NU + 6 * jk;
       if (jc == 0) acc += wk[0] - wk[1] + wk[2] - wk[3];
@@ -468,164 +610,281 @@ __global__ __launch_bounds__(kWave) void osc_solve_kernel(
     }
     return acc;
   };
-  // K = Hr + G' diag(Dr) G, column j in registers; also records the diagonal in sDg.
-  auto assemble = [&](double (&c)[NY]) {
-    const int jj = (j < NY) ? j : 0;
+  // contact block column (B[0..2][jc]) of var slot in contact jk, from D = lambda/s
+  auto contact_col = [&](int jk, int jc, double& v0, double& v1_, double& v2) {
+    const double* dk = sDr + 2 * NU + 6 * jk;
+    const double s4 = dk[0] + dk[1] + dk[2] + dk[3];
+    const double sxy = dk[0] - dk[1] - dk[2] + dk[3];
+    const double sx = dk[0] - dk[1] + dk[2] - dk[3];
+    const double sy = dk[0] + dk[1] - dk[2] - dk[3];
+    const double b00 = s4, b11 = s4, b01 = sxy, b02 = -mu_f * sx, b12 = -mu_f * sy,
+                 b22 = mu_f * mu_f * s4 + dk[4] + dk[5];
+    v0 = (jc == 0) ? b00 : (jc == 1) ? b01 : b02;
+    v1_ = (jc == 0) ? b01 : (jc == 1) ? b11 : b12;
+    v2 = (jc == 0) ? b02 : (jc == 1) ? b12 : b22;
+  };
+
+  double c0[NY], c1[NY];
+  double dinv0, dinv1;
+  // Hr columns j0, j1 (and their diagonal entries) -> registers; re-issued at the end of every
+  // iteration so the loads fly while the step is applied and the next residuals are formed.
+  auto load_hr = [&]() {
 #pragma unroll
-    for (int i = 0; i < NY; ++i) c[i] = sHr[i * NY + jj];
-    double dg = sHr[jj * NY + jj];
+    for (int i = 0; i < NY; ++i) {
+      c0[i] = gHr[i * NY + j0];
+      c1[i] = gHr[i * NY + jj1];
+    }
+  };
+  const double hdg0 = gHr[j0 * NY + j0], hdg1 = gHr[jj1 * NY + jj1];
+  load_hr();
+  const double g0 = sG[j0], g1 = sG[jj1];
+  double y0 = 0.0, y1 = 0.0;
+  double s[NRL], lam[NRL];
+#pragma unroll
+  for (int t = 0; t < NRL; ++t) {
+    s[t] = 1.0;
+    lam[t] = 0.0;
+  }
+  double nact = 0.0;
+#pragma unroll
+  for (int t = 0; t < NRL; ++t) nact += act[t] ? 1.0 : 0.0;
+  const double m_act = row_sum(nact);
+  bool done = !valid;
+  int32_t st = OSC_SOLVE_MAX_ITER;
+  int it_done = 0;
+
+  // One loop body for everything, so factorisation and solve code exist once (I-cache).
+  // it == -1 builds the initial point (Mehrotra-style):
+  //   (Hr + G'G) y0 = -g + G'h,  s = h - G y0,  lambda = G y0 - h,  both shifted positive.
+  // The four environments of the wave iterate in lockstep; a converged one stops moving
+  // (step 0) until the slowest has converged.
+  for (int it = -1;; ++it) {
+    STAMP_BEGIN();
+    const bool init = it < 0;
+    double rp[NRL];
+    double mu = 0.0;
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) rp[t] = 0.0;
+    if (!init) {
+      uv_product(sVy);
+      wave_sync();
+      double cs = 0.0;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        rp[t] = act[t] ? Gv(sVy, t) + s[t] - h[t] : 0.0;
+        cs += act[t] ? s[t] * lam[t] : 0.0;
+      }
+      mu = row_sum(cs) / fmax(m_act, 1.0);
+      if (!done && mu <= P->eps_mu) {
+        done = true;
+        st = OSC_SOLVE_OK;
+        it_done = it;
+      }
+      if (__ballot(!done) == 0 || it >= P->max_iter) {
+        if (!done) it_done = it;
+        break;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) {
+      const int r = l + kRow * t;
+      sVr[r] = init ? 0.0 : (act[t] ? lam[t] : 0.0);
+      sDr[r] = act[t] ? (init ? 1.0 : lam[t] * recip(s[t])) : 0.0;
+    }
+    wave_sync();
+
+    STAMP_END(1);
+    STAMP_BEGIN();
+    // ---- Newton matrix K = Hr + G' D G (columns j0, j1 in registers) and rd = Hr y + g + G'lam
+    double rd0 = g0 + GTw(sVr, j0, jk0, jc0), rd1 = g1 + GTw(sVr, jj1, jk1, jc1);
+    double dg0 = hdg0, dg1 = hdg1;
+    if (!init) {
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        rd0 = fma(c0[i], sVy[i], rd0);
+        rd1 = fma(c1[i], sVy[i], rd1);
+      }
+    }
 #pragma unroll 1
     for (int q = 0; q < NU; ++q) {   // rolled: bounds the number of U loads in flight
       const double du = sDr[2 * q] + sDr[2 * q + 1];
-      const double uj = sU[q * NY1 + jj];
-      const double t = du * uj;
-      dg = fma(t, uj, dg);
+      const double u0 = sU[q * NY1P + j0], u1 = sU[q * NY1P + jj1];
+      const double t0 = du * u0, t1 = du * u1;
+      dg0 = fma(t0, u0, dg0);
+      dg1 = fma(t1, u1, dg1);
 #pragma unroll
-      for (int i = 0; i < NY; ++i) c[i] = fma(t, sU[q * NY1 + i], c[i]);
+      for (int i = 0; i < NY; ++i) {
+        const double uqi = sU[q * NY1P + i];
+        c0[i] = fma(t0, uqi, c0[i]);
+        c1[i] = fma(t1, uqi, c1[i]);
+      }
     }
-    if (jk >= 0) {
-      const double* dk = sDr + 2 * NU + 6 * jk;
-      const double s4 = dk[0] + dk[1] + dk[2] + dk[3];
-      const double sxy = dk[0] - dk[1] - dk[2] + dk[3];
-      const double sx = dk[0] - dk[1] + dk[2] - dk[3];
-      const double sy = dk[0] + dk[1] - dk[2] - dk[3];
-      const double b00 = s4, b11 = s4, b01 = sxy, b02 = -mu_f * sx, b12 = -mu_f * sy,
-                   b22 = mu_f * mu_f * s4 + dk[4] + dk[5];
-      const double v0 = (jc == 0) ? b00 : (jc == 1) ? b01 : b02;
-      const double v1 = (jc == 0) ? b01 : (jc == 1) ? b11 : b12;
-      const double v2 = (jc == 0) ? b02 : (jc == 1) ? b12 : b22;
-      dg += (jc == 0) ? v0 : (jc == 1) ? v1 : v2;
+    if (jk0 >= 0) {
+      double a, b, cc;
+      contact_col(jk0, jc0, a, b, cc);
+      dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
 #pragma unroll
       for (int i = NU; i < NY; ++i) {
         const int ki = (i - NU) / 3, ci = (i - NU) % 3;
-        const double add = (ci == 0) ? v0 : (ci == 1) ? v1 : v2;
-        c[i] += (ki == jk) ? add : 0.0;
+        c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
       }
     }
-    if (j < NY) sDg[j] = dg;
-    __syncthreads();
-  };
-
-  double c[NY];
-  double dinv;
-  const double gj = (j < NY) ? sG[j] : 0.0;
-  int32_t st = OSC_SOLVE_MAX_ITER;
-  int it;
-  const double m_act = wave_sum(act ? 1.0 : 0.0);   // active rows (wave-uniform)
-  double yj = 0.0, s = 1.0, lam = 0.0;
-
-  // One loop body for everything, so the factorisation and solve code exist once in the
-  // binary (I-cache).  it == -1 builds the initial point (Mehrotra-style):
-  //   (Hr + G'G) y0 = -g + G'h,   s = h - G y0,  lambda = G y0 - h,  both shifted positive.
-  for (it = -1;; ++it) {
-    const bool init = it < 0;
-    double rp = 0.0, rd = gj, mu = 0.0;
-    if (init) {
-      sDr[r] = act ? 1.0 : 0.0;
-    } else {
-      const double gy = Gv(sVy);
-      rp = act ? gy + s - h : 0.0;
-      mu = wave_sum(act ? s * lam : 0.0) / m_act;
-      if (mu <= P->eps_mu) {
-        st = OSC_SOLVE_OK;
-        break;
-      }
-      if (it >= P->max_iter) break;
-      // dual residual rd = Hr y + g + G' lambda ;  D = lambda / s
-      sVr[r] = act ? lam : 0.0;
-      sDr[r] = act ? lam / s : 0.0;
-      __syncthreads();
-      rd += GTw(sVr);
-      if (j < NY) {
+    if (jk1 >= 0) {
+      double a, b, cc;
+      contact_col(jk1, jc1, a, b, cc);
+      dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
 #pragma unroll
-        for (int i = 0; i < NY; ++i) rd = fma(sHr[i * NY + j], sVy[i], rd);
+      for (int i = NU; i < NY; ++i) {
+        const int ki = (i - NU) / 3, ci = (i - NU) % 3;
+        c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
       }
     }
-    __syncthreads();
-    assemble(c);
-    ldl_columns<NY>(c, dinv, sDg, sDinv, lane);
+    sDg[j0] = dg0;
+    if (v1) sDg[j1] = dg1;
+    wave_sync();
+    STAMP_END(2);
+    STAMP_BEGIN();
+    ldl_rows<NY>(c0, c1, dinv0, dinv1, sDg, sDinv, l);
+    wave_sync();
+    STAMP_END(3);
 
     // pass 0: affine (predictor) direction, rc = s lambda
     // pass 1: corrector, rc = s lambda + ds_aff dl_aff - sigma mu
-    double ds = 0.0, dl = 0.0, dyj = 0.0, gdy = 0.0, ds_a = 0.0, dl_a = 0.0, sig_mu = 0.0,
-           step = 1.0;
+    double ds[NRL], dl[NRL], dsdl[NRL];
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) ds[t] = dl[t] = dsdl[t] = 0.0;
+    double dy0 = 0.0, dy1 = 0.0, sig_mu = 0.0, step = 1.0;
     const int npass = init ? 1 : 2;
     for (int pass = 0; pass < npass; ++pass) {
-      const double rcv = (pass == 0) ? s * lam : fma(ds_a, dl_a, s * lam) - sig_mu;
-      sVr[r] = init ? (act ? h : 0.0) : (act ? (rcv - lam * rp) / s : 0.0);
-      __syncthreads();
-      dyj = ldl_solve<NY>(c, dinv, sDinv, -rd + GTw(sVr), lane);
-      if (j < NY) sVy2[j] = dyj;
-      __syncthreads();
-      gdy = Gv(sVy2);
-      ds = act ? -rp - gdy : 0.0;
-      dl = act ? -(rcv + lam * ds) / s : 0.0;
+      STAMP_BEGIN();
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        const double rc = fma(s[t], lam[t], dsdl[t]) - sig_mu;   // dsdl = sig_mu = 0 in pass 0
+        sVr[l + kRow * t] =
+            init ? (act[t] ? h[t] : 0.0) : (act[t] ? (rc - lam[t] * rp[t]) * recip(s[t]) : 0.0);
+      }
+      wave_sync();
+      dy0 = -rd0 + GTw(sVr, j0, jk0, jc0);
+      dy1 = -rd1 + GTw(sVr, jj1, jk1, jc1);
+      STAMP_END(4);
+      STAMP_BEGIN();
+      ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, sDinv, dy0, dy1, l);
+      sVy2[j0] = dy0;
+      if (v1) sVy2[j1] = dy1;
+      wave_sync();
+      STAMP_END(5);
+      STAMP_BEGIN();
+      uv_product(sVy2);
+      wave_sync();
       double ratio = 1.0;
-      if (act) {
-        if (ds < 0.0) ratio = fmin(ratio, -s / ds);
-        if (dl < 0.0) ratio = fmin(ratio, -lam / dl);
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        const double rc = fma(s[t], lam[t], dsdl[t]) - sig_mu;
+        const double gdy = Gv(sVy2, t);
+        ds[t] = act[t] ? -rp[t] - gdy : 0.0;
+        dl[t] = act[t] ? -(rc + lam[t] * ds[t]) * recip(s[t]) : 0.0;
+        if (act[t]) {
+          if (ds[t] < 0.0) ratio = fmin(ratio, -s[t] * recip(ds[t]));
+          if (dl[t] < 0.0) ratio = fmin(ratio, -lam[t] * recip(dl[t]));
+        }
       }
-      step = wave_min(ratio);
+      step = row_min(ratio);
       if (pass == 0 && !init) {
-        const double mu_aff = wave_sum(act ? (s + step * ds) * (lam + step * dl) : 0.0) / m_act;
-        const double q = mu_aff / mu;
+        double ca = 0.0;
+#pragma unroll
+        for (int t = 0; t < NRL; ++t)
+          ca += act[t] ? (s[t] + step * ds[t]) * (lam[t] + step * dl[t]) : 0.0;
+        const double mu_aff = row_sum(ca) / fmax(m_act, 1.0);
+        const double q = mu_aff / fmax(mu, 1e-300);
         sig_mu = q * q * q * mu;
-        ds_a = ds;
-        dl_a = dl;
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) dsdl[t] = ds[t] * dl[t];
       }
-      __syncthreads();
+      wave_sync();
+      STAMP_END(6);
     }
+    STAMP_BEGIN();
     if (init) {
-      yj = dyj;
-      const double zr = gdy - h;
-      const double ap = wave_max(act ? zr : -1e300);    // = max(-s)
-      const double ad = wave_max(act ? -zr : -1e300);   // = max(-lambda)
-      s = act ? ((ap >= 0.0) ? -zr + 1.0 + ap : -zr) : 1.0;
-      lam = act ? ((ad >= 0.0) ? zr + 1.0 + ad : zr) : 0.0;
+      // here rp = 0, so ds = -G y0 and  G y0 - h = -ds - h
+      y0 = dy0;
+      y1 = dy1;
+      double zmax = -1e300, nzmax = -1e300;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        const double zr = -ds[t] - h[t];
+        if (act[t]) {
+          zmax = fmax(zmax, zr);
+          nzmax = fmax(nzmax, -zr);
+        }
+      }
+      const double ap = row_max(zmax);    // = max(-s)
+      const double ad = row_max(nzmax);   // = max(-lambda)
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        const double zr = -ds[t] - h[t];
+        s[t] = act[t] ? ((ap >= 0.0) ? -zr + 1.0 + ap : -zr) : 1.0;
+        lam[t] = act[t] ? ((ad >= 0.0) ? zr + 1.0 + ad : zr) : 0.0;
+      }
+      if (m_act == 0.0 && !done) {        // unconstrained: y0 = -Hr^-1 g is the optimum
+        done = true;
+        st = OSC_SOLVE_OK;
+        it_done = 0;
+      }
     } else {
-      const double alpha = fmin(1.0, 0.99 * step);
-      yj = fma(alpha, dyj, yj);
-      s = act ? fma(alpha, ds, s) : 1.0;
-      lam = act ? fma(alpha, dl, lam) : 0.0;
+      const double alpha = done ? 0.0 : fmin(1.0, 0.99 * step);
+      y0 = fma(alpha, dy0, y0);
+      y1 = fma(alpha, dy1, y1);
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        s[t] = act[t] ? fma(alpha, ds[t], s[t]) : 1.0;
+        lam[t] = act[t] ? fma(alpha, dl[t], lam[t]) : 0.0;
+      }
     }
-    if (j < NY) sVy[j] = yj;
-    __syncthreads();
-    if (init && m_act == 0.0) {   // unconstrained: y0 = -Hr^-1 g is the optimum
-      st = OSC_SOLVE_OK;
-      it = 0;
-      break;
-    }
+    sVy[j0] = y0;
+    if (v1) sVy[j1] = y1;
+    load_hr();   // next iteration's Hr columns (the factor in c0/c1 is dead now)
+    wave_sync();
+    STAMP_END(7);
   }
+  STAMP_STORE();
 
   // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
-  double tq = 0.0;
-  if (lane < NU) {
-    tq = sU[lane * NY1 + NY];
+  if (l < NU) {
+    double tq = sU[l * NY1P + NY];
 #pragma unroll
-    for (int i = 0; i < NY; ++i) tq = fma(sU[lane * NY1 + i], sVy[i], tq);
-    sTau[lane] = tq;
+    for (int i = 0; i < NY; ++i) tq = fma(sU[l * NY1P + i], sVy[i], tq);
+    sTau[l] = tq;
+    if (valid) gtau[static_cast<size_t>(env) * NU + l] = tq;
   }
-  double xb = 0.0;
-  if (lane < NB) {
-    xb = sX[lane * NY1 + NY];
+  if (gx != nullptr && l < NB) {
+    const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + l * NY1P;
+    double xb = xr[NY];
 #pragma unroll
-    for (int i = 0; i < NY; ++i) xb = fma(sX[lane * NY1 + i], sVy[i], xb);
+    for (int i = 0; i < NY; ++i) xb = fma(xr[i], sVy[i], xb);
+    sXb[l] = xb;
   }
-  __syncthreads();
-  const bool finite = wave_min((lane < NY) ? (isfinite(yj) ? 1.0 : 0.0) : 1.0) > 0.0;
-  if (!finite) st = OSC_SOLVE_NUMERICAL;
-  if (lane < NU) gtau[static_cast<size_t>(env) * NU + lane] = tq;
-  if (gx != nullptr && lane < D::NX) {
-    double v;
-    if (lane < NB) v = xb;
-    else if (lane < NV) v = sVy[lane - NB];
-    else if (lane < NV + NU) v = sTau[lane - NV];
-    else v = sVy[NU + lane - NV - NU];
-    gx[static_cast<size_t>(env) * D::NX + lane] = v;
-  }
-  if (lane == 0) {
-    if (gstatus) gstatus[env] = st;
-    if (giters) giters[env] = it;
+  wave_sync();
+  const double fin = (isfinite(y0) && (!v1 || isfinite(y1))) ? 1.0 : 0.0;
+  if (row_min(fin) == 0.0) st = OSC_SOLVE_NUMERICAL;
+  if (valid) {
+    if (gx != nullptr) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int idx = l + kRow * t;
+        if (idx < D::NX) {
+          double v;
+          if (idx < NB) v = sXb[idx];
+          else if (idx < NV) v = sVy[idx - NB];
+          else if (idx < NV + NU) v = sTau[idx - NV];
+          else v = sVy[NU + idx - NV - NU];
+          gx[static_cast<size_t>(env) * D::NX + idx] = v;
+        }
+      }
+    }
+    if (l == 0) {
+      if (gstatus) gstatus[env] = st;
+      if (giters) giters[env] = it_done;
+    }
   }
 }
 
@@ -639,6 +898,14 @@ KernelId select_kernel(const osc_model_desc& d) {
   if (d.nv == Walter::NV && d.nu == Walter::NU && d.nc == Walter::NC && d.ns == Walter::NS)
     return K_WALTER;
   return K_NONE;
+}
+
+int ws_doubles(KernelId k) {
+  switch (k) {
+    case K_GO2: return Go2::WS;
+    case K_WALTER: return Walter::WS;
+    default: return 0;
+  }
 }
 
 }  // namespace
@@ -729,61 +996,107 @@ extern "C" int osc_model_get_desc(const osc_model* model, osc_model_desc* desc) 
   return OSC_OK;
 }
 
+extern "C" int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes) {
+  if (!model || !bytes || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+  *bytes = sizeof(double) * static_cast<size_t>(ws_doubles(model->kid)) * static_cast<size_t>(nenv);
+  return OSC_OK;
+}
+
 namespace {
+
+template <class D>
+int launch_t(const osc_model* model, int32_t nenv, const double* M, const double* C,
+             const double* J, const double* b, const double* T, const double* mask, double* tau,
+             double* x, int32_t* status, int32_t* iters, double* ws, hipStream_t s,
+             bool setup_only) {
+  hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
+                     model->dparams, nenv, M, C, J, b, T, mask, ws);
+  if (!setup_only) {
+    const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
+    hipLaunchKernelGGL(osc_ipm_kernel<D>, dim3(nb), dim3(kWave), 0, s, model->dparams, nenv,
+                       mask, ws, tau, x, status, iters);
+  }
+  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+
 int launch(const osc_model* model, int32_t nenv, const double* M, const double* C, const double* J,
            const double* b, const double* T, const double* contact_mask, double* tau, double* x,
-           int32_t* status, int32_t* iters, void* stream, double* dbg) {
+           int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes,
+           void* stream, bool setup_only) {
   if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
   if (nenv == 0) return OSC_OK;
-  if (!M || !C || !J || !b || !T || !contact_mask || !tau) return OSC_ERR_INVALID_ARGUMENT;
+  if (!M || !C || !J || !b || !T || !contact_mask || (!tau && !setup_only))
+    return OSC_ERR_INVALID_ARGUMENT;
   // 16-byte alignment is required by the vectorised staging loads.
   const uintptr_t align = reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(C) |
                           reinterpret_cast<uintptr_t>(J) | reinterpret_cast<uintptr_t>(b) |
                           reinterpret_cast<uintptr_t>(T) |
-                          reinterpret_cast<uintptr_t>(contact_mask);
+                          reinterpret_cast<uintptr_t>(contact_mask) |
+                          reinterpret_cast<uintptr_t>(workspace);
   if (align & 15u) return OSC_ERR_INVALID_ARGUMENT;
+  size_t need = 0;
+  osc_workspace_bytes(model, nenv, &need);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid(static_cast<unsigned>(nenv)), block(kWave);
+  double* ws = static_cast<double*>(workspace);
+  bool owned = false;
+  if (ws == nullptr) {   // convenience path: stream-ordered scratch
+    if (hipMallocAsync(reinterpret_cast<void**>(&ws), need, s) != hipSuccess) return OSC_ERR_DEVICE;
+    owned = true;
+  } else if (workspace_bytes < need) {
+    return OSC_ERR_INVALID_ARGUMENT;
+  }
+  int rc;
   switch (model->kid) {
     case K_GO2:
-      hipLaunchKernelGGL(osc_solve_kernel<Go2>, grid, block, 0, s, model->dparams, nenv, M, C, J,
-                         b, T, contact_mask, tau, x, status, iters, dbg);
+      rc = launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s,
+                         setup_only);
       break;
     case K_WALTER:
-      hipLaunchKernelGGL(osc_solve_kernel<Walter>, grid, block, 0, s, model->dparams, nenv, M, C,
-                         J, b, T, contact_mask, tau, x, status, iters, dbg);
+      rc = launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws,
+                            s, setup_only);
       break;
     default:
-      return OSC_ERR_UNSUPPORTED_DIMS;
+      rc = OSC_ERR_UNSUPPORTED_DIMS;
   }
-  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+  if (owned) (void)hipFreeAsync(ws, s);
+  return rc;
 }
+
 }  // namespace
 
 extern "C" int osc_batch_solve(const osc_model* model, int32_t nenv, const double* M,
                                const double* C, const double* J, const double* b, const double* T,
                                const double* contact_mask, double* tau, double* x,
-                               int32_t* status, int32_t* iters, void* stream) {
-  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, stream, nullptr);
+                               int32_t* status, int32_t* iters, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
+                workspace_bytes, stream, false);
 }
 
-// Test hook, not part of include/osc_batch.h: same solve, plus a per-env dump of the reduced QP
-// [Hr (NY x NY) | g (NY) | U (NU x (NY+1)) | X (NB x (NY+1))] into `dbg` (device pointer,
-// osc_debug_dump_size() doubles per env).  Used by tests/test_gpu_stages.py.
+#ifdef OSC_STAMPS
+// Diagnostic build only: per-block IPM phase cycles [nblocks][8] (see STAMP_* above).
+extern "C" int osc_debug_stamps(unsigned long long* host, int nblocks) {
+  if (nblocks > kStampBlocks) nblocks = kStampBlocks;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kStampSlots *
+                             nblocks) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+#endif
+
+// Test hook, not part of include/osc_batch.h: run only the setup kernel and leave the reduced
+// QP [Hr (NY x NY) | g (NY, padded even) | U (NU x NY1P) | X (NB x NY1P)] of every env in
+// `dbg` (device pointer, osc_debug_dump_size() doubles per env).  tests/test_gpu_stages.py.
 extern "C" int osc_debug_dump_size(const osc_model* model) {
   if (!model) return -1;
-  switch (model->kid) {
-    case K_GO2: return Go2::DBG;
-    case K_WALTER: return Walter::DBG;
-    default: return -1;
-  }
+  return ws_doubles(model->kid);
 }
 
 extern "C" int osc_debug_reduced_qp(const osc_model* model, int32_t nenv, const double* M,
                                     const double* C, const double* J, const double* b,
-                                    const double* T, const double* contact_mask, double* tau,
-                                    double* dbg, void* stream) {
+                                    const double* T, const double* contact_mask, double* dbg,
+                                    void* stream) {
   if (!dbg) return OSC_ERR_INVALID_ARGUMENT;
-  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, nullptr, nullptr, nullptr, stream,
-                dbg);
+  size_t need = 0;
+  if (osc_workspace_bytes(model, nenv, &need) != OSC_OK) return OSC_ERR_INVALID_ARGUMENT;
+  return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
+                dbg, need, stream, true);
 }

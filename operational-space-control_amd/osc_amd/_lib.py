@@ -10,7 +10,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libosc_batch.so")
+LIB_PATH = os.environ.get("OSC_LIB_PATH", os.path.join(PKG_DIR, "lib", "libosc_batch.so"))
 
 OSC_MAX_SITES = 32
 OSC_MAX_NU = 16
@@ -20,8 +20,8 @@ STATUS_NAMES = {0: "OSC_OK", 1: "OSC_ERR_INVALID_ARGUMENT", 2: "OSC_ERR_UNSUPPOR
 SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL = 0, 1, 2
 
 EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
-                    "osc_model_destroy", "osc_model_get_desc", "osc_batch_solve",
-                    "osc_status_string", "osc_abi_version")
+                    "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
+                    "osc_batch_solve", "osc_status_string", "osc_abi_version")
 
 
 class OscModelDesc(ctypes.Structure):
@@ -69,7 +69,9 @@ def lib() -> ctypes.CDLL:
     L.osc_model_destroy.restype = ctypes.c_int
     L.osc_model_get_desc.argtypes = [vp, dp]
     L.osc_model_get_desc.restype = ctypes.c_int
-    L.osc_batch_solve.argtypes = [vp, i32] + [vp] * 10 + [vp]
+    L.osc_workspace_bytes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t)]
+    L.osc_workspace_bytes.restype = ctypes.c_int
+    L.osc_batch_solve.argtypes = [vp, i32] + [vp] * 10 + [vp, ctypes.c_size_t, vp]
     L.osc_batch_solve.restype = ctypes.c_int
     L.osc_status_string.argtypes = [ctypes.c_int]
     L.osc_status_string.restype = ctypes.c_char_p
@@ -78,7 +80,7 @@ def lib() -> ctypes.CDLL:
     # test hooks (not in the public header)
     L.osc_debug_dump_size.argtypes = [vp]
     L.osc_debug_dump_size.restype = ctypes.c_int
-    L.osc_debug_reduced_qp.argtypes = [vp, i32] + [vp] * 9
+    L.osc_debug_reduced_qp.argtypes = [vp, i32] + [vp] * 8
     L.osc_debug_reduced_qp.restype = ctypes.c_int
     _lib = L
     return L

@@ -30,6 +30,7 @@ class SolveResult:
     x: torch.Tensor | None     # (nenv, nv + nu + 3nc) design vector (dv, u, z)
     status: torch.Tensor       # (nenv,) int32, 0 = converged
     iters: torch.Tensor        # (nenv,) int32, interior-point iterations
+    workspace: torch.Tensor | None = None   # device scratch (reduced QP per env)
 
 
 class OSCBatchSolver:
@@ -82,7 +83,12 @@ class OSCBatchSolver:
         x = torch.empty((nenv, d["n"]), dtype=torch.float64, **opts) if want_x else None
         status = torch.empty((nenv,), dtype=torch.int32, **opts)
         iters = torch.empty((nenv,), dtype=torch.int32, **opts)
-        return SolveResult(tau, x, status, iters)
+        nb = ctypes.c_size_t()
+        rc = _lib.lib().osc_workspace_bytes(self._h, nenv, ctypes.byref(nb))
+        if rc != 0:
+            raise _lib.OSCError("osc_workspace_bytes", rc)
+        ws = torch.empty((max(nb.value // 8, 2),), dtype=torch.float64, **opts)
+        return SolveResult(tau, x, status, iters, ws)
 
     def solve_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None) -> SolveResult:
         """Launch only (no allocation, no host sync): the benchmarked call."""
@@ -91,7 +97,10 @@ class OSCBatchSolver:
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         rc = _lib.lib().osc_batch_solve(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
                                         ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
-                                        ptr(out.iters), ctypes.c_void_p(s))
+                                        ptr(out.iters), ptr(out.workspace),
+                                        ctypes.c_size_t(0 if out.workspace is None else
+                                                        out.workspace.numel() * 8),
+                                        ctypes.c_void_p(s))
         if rc != 0:
             raise _lib.OSCError("osc_batch_solve", rc)
         return out

@@ -69,7 +69,7 @@ def test_error_codes():
     d = _lib.desc_from_yaml("unitree_go2")
     d.z_ub[0] = 5.0                             # finite fx bound: not in the reference QP
     assert L.osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 1
-    assert L.osc_batch_solve(None, 1, *([None] * 10), None) == 1
+    assert L.osc_batch_solve(None, 1, *([None] * 10), None, 0, None) == 1
     assert L.osc_model_destroy(None) == 1
 
 

@@ -134,11 +134,21 @@ def test_edge_cases(gpu):
     d = generate("unitree_go2", 4, SEED_BASE + 11, "standing", "ones")
     # empty batch is a no-op
     from osc_amd import _lib
-    assert _lib.lib().osc_batch_solve(s._h, 0, *([None] * 10), None) == 0
+    assert _lib.lib().osc_batch_solve(s._h, 0, *([None] * 10), None, 0, None) == 0
+    # the convenience path without a caller workspace gives identical results
+    import ctypes
+    args = s.prepare(**d)
+    out = s.alloc_outputs(4)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = _lib.lib().osc_batch_solve(s._h, 4, *[p(a) for a in args], p(out.tau), None, p(out.status),
+                                    p(out.iters), None, 0,
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
     # single env matches its row in a batch
     res4 = s.solve(**d)
     res1 = s.solve(**{k: v[1:2] for k, v in d.items()})
     torch.cuda.synchronize()
+    assert torch.equal(out.tau, res4.tau)
     assert torch.equal(res1.tau[0], res4.tau[1])
     # a NaN input poisons only its own environment, and says so
     d2 = {k: v.copy() for k, v in d.items()}

@@ -35,11 +35,15 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     args = s.prepare(**inp)
     L = _lib.lib()
     sz = L.osc_debug_dump_size(s._h)
-    assert sz == ny * ny + ny + nu * (ny + 1) + nb * (ny + 1)
+    ev = lambda a: (a + 1) // 2 * 2
+    ny1p = ev(ny + 1)
+    o_g, o_u = 0, ev(ny)
+    o_hr = o_u + nu * ny1p
+    o_x = o_hr + ev(ny * ny)
+    assert sz == o_x + nb * ny1p
     dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
-    tau = torch.empty((nenv, nu), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
-    rc = L.osc_debug_reduced_qp(s._h, nenv, *[p(a) for a in args], p(tau), p(dbg),
+    rc = L.osc_debug_reduced_qp(s._h, nenv, *[p(a) for a in args], p(dbg),
                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     assert rc == 0
     torch.cuda.synchronize()
@@ -47,10 +51,10 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     model = load_model(robot)
     rng = np.random.default_rng(0)
     for e in range(nenv):
-        Hr = D[e, :ny * ny].reshape(ny, ny)
-        g = D[e, ny * ny:ny * ny + ny]
-        U = D[e, ny * ny + ny:ny * ny + ny + nu * (ny + 1)].reshape(nu, ny + 1)
-        X = D[e, ny * ny + ny + nu * (ny + 1):].reshape(nb, ny + 1)
+        Hr = D[e, o_hr:o_hr + ny * ny].reshape(ny, ny)
+        g = D[e, o_g:o_g + ny]
+        U = D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
+        X = D[e, o_x:].reshape(nb, ny1p)[:, :ny + 1]
         np.testing.assert_array_equal(Hr, Hr.T)
         a = [inp[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a)

@@ -173,6 +173,50 @@ __global__ __launch_bounds__(64) void v4(double* out) {
   out[blockIdx.x * 64 + lane] = acc;
 }
 
+
+// V5: 4 envs / wave, one 16-lane DPP row per env, 2 columns per lane, pivot column broadcast
+// with v_mov_b64_dpp row_newbcast (VALU, no LDS pipe), reciprocal by rcp + 2 Newton steps.
+template <int K>
+__device__ __forceinline__ double rowb(double v) {
+  long long x = __double_as_longlong(v);
+  return __longlong_as_double(__builtin_amdgcn_mov_dpp(x, 0x150 + K, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+template <int N, int REPS>
+__global__ __launch_bounds__(64) void v5(double* out) {
+  const int lane = threadIdx.x, l = lane & 15;
+  double c0[N], c1[N];
+  double acc = 0;
+  for (int rep = 0; rep < REPS; ++rep) {
+    init_col<N>(c0, l, rep);
+    init_col<N>(c1, l + 16, rep);
+    static_for<0, N>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      double dk;
+      if constexpr (k < 16) dk = rowb<k % 16>(c0[k]); else dk = rowb<k % 16>(c1[k]);
+      const double inv = recip(dk);
+      const int ln = opaque(l);
+      const double t0 = (ln > k && ln < N) ? -c0[k] * inv : 0.0;
+      const double t1 = (ln + 16 > k && ln + 16 < N) ? -c1[k] * inv : 0.0;
+      static_for<k + 1, N>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        double b;
+        if constexpr (k < 16) b = rowb<k % 16>(c0[i]); else b = rowb<k % 16>(c1[i]);
+        c0[i] = fma(b, t0, c0[i]);
+        if constexpr (N > 16) c1[i] = fma(b, t1, c1[i]);
+      });
+    });
+    acc += c0[N - 1] + c1[N - 1];
+  }
+  out[blockIdx.x * 64 + lane] = acc;
+}
+
 template <class F>
 float time_it(F kern, int blocks, double* out) {
   hipEvent_t a, b;
@@ -199,10 +243,11 @@ void run() {
   float t3 = time_it(v3<N, REPS>, blocks, out);
   float t4 = time_it(v4<N, REPS>, blocks, out);
   float t2b = time_it(v2b<N, REPS>, blocks, out);
+  float t5 = time_it(v5<N, REPS>, blocks, out);
   auto per = [&](float ms, int envs_per_wave) { return ms * 1e6 / (double(blocks) * envs_per_wave * REPS); };
   printf("{\"N\": %d, \"ns_per_env_ldl\": {\"v1_readlane_1env\": %.3f, \"v2_swizzle_2env\": %.3f, "
-         "\"v3_readlane_2env\": %.3f, \"v4_swizzle_4env\": %.3f, \"v2b_bpermute_2env\": %.3f}}\n",
-         N, per(t1, 1), per(t2, 2), per(t3, 2), per(t4, 4), per(t2b, 2));
+         "\"v3_readlane_2env\": %.3f, \"v4_swizzle_4env\": %.3f, \"v2b_bpermute_2env\": %.3f, \"v5_dpp_4env\": %.3f}}\n",
+         N, per(t1, 1), per(t2, 2), per(t3, 2), per(t4, 4), per(t2b, 2), per(t5, 4));
   hipFree(out);
 }
 

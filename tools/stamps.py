@@ -1,0 +1,40 @@
+"""Diagnostic: per-phase cycle shares of the IPM kernel from the OSC_STAMPS build
+(lib/libosc_batch_stamps.so).  Stamps serialise the wave, so read SHARES, not absolute time."""
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["OSC_LIB_PATH"] = os.path.join(REPO, "operational-space-control_amd", "lib",
+                                          "libosc_batch_stamps.so")
+sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from osc_amd import _lib  # noqa: E402
+from osc_amd.solver import OSCBatchSolver  # noqa: E402
+from osc_amd.synth import SEED_BASE, generate  # noqa: E402
+
+NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble K", "LDL^T", "rhs (2 passes)",
+         "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update"]
+for robot in ["unitree_go2", "walter_sr"]:
+    nenv = 16384
+    s = OSCBatchSolver(robot)
+    d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
+    args = s.prepare(**d)
+    out = s.alloc_outputs(nenv)
+    s.solve_into(out, *args)
+    torch.cuda.synchronize()
+    nblk = nenv // 4
+    buf = (ctypes.c_ulonglong * (nblk * 8))()
+    L = _lib.lib()
+    L.osc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert L.osc_debug_stamps(ctypes.cast(buf, ctypes.c_void_p), nblk) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, 8).astype(np.float64)
+    it = out.iters.cpu().numpy().reshape(nblk, 4).max(axis=1) + 1   # + init pass
+    tot = a.sum(axis=1)
+    per = {n: float(a[:, k].mean()) for k, n in enumerate(NAMES)}
+    print(json.dumps({"robot": robot, "mean_cycles_per_wave": float(tot.mean()),
+                      "mean_wave_iters": float(it.mean()),
+                      "cycles_per_wave_iter": float((tot / it).mean()),
+                      "share": {n: round(per[n] / tot.mean(), 3) for n in NAMES}}), flush=True)
