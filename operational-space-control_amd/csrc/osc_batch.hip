@@ -429,22 +429,52 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
 
 // ============================ kernel 2: interior point, 4 env / wave ========================
 
+// c += bcast_K(src) * m  in ONE instruction: v_fmac_f64_dpp with row_newbcast:K (the DPP
+// operand is read from lane K of each 16-lane row).  hipcc never forms this (64-bit DPP is
+// only legal with row_newbcast), hence inline asm.  The compiler's hazard recognizer cannot see
+// through inline asm, so every DPP read here carries its own guard: NOP = true prefixes
+// s_nop 1 (gfx9: a VALU write of the DPP source needs 2 wait states before the DPP read) for a
+// source just computed by the caller; NOP = false only where the source was written by one of
+// these asm statements several dependent instructions earlier.
+template <int K, bool NOP = false>
+__device__ __forceinline__ void fmac_bcast(double& c, double src, double m) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
+}
+template <int K>
+__device__ __forceinline__ void fmac_bcast_self(double& c, double m) {
+  asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "+v"(c) : "v"(m), "n"(K));
+}
+// Broadcast of lane K's v within each 16-lane row, guarded (v may have been written by asm).
+template <int K>
+__device__ __forceinline__ double bcast_guarded(double v) {
+  double r;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "=v"(r) : "v"(v), "n"(K));
+  return r;
+}
+
 // LDL^T of an N x N symmetric matrix held one column per lane in two slots: lane l of a row
-// holds column l in c0 and column l+16 in c1.  On exit (for slot column j):
-//   c[i], i > j : L[i][j]            (unit lower factor, column j)
+// holds column l in c0 and column l+16 in c1.  Right-looking; at step k every lane j > k
+// applies  c_j[i] -= L[i][k] L[j][k] D_k  for i > k with the pivot column entry c_k[i]
+// broadcast by DPP straight into the FMA.  On exit (for slot column j):
+//   c[i], i > j : L[i][j] * D[j]     (column j of L, unscaled)
 //   c[i], i < j : L[j][i] * D[i]     (row j of L, scaled -- left by the symmetric update)
-//   dinv        : 1 / D[j]
-// sdg: original diagonal (Cholesky-infinity test); sdinv receives 1/D for the solves.
+//   d, dinv     : D[j], 1 / D[j]
+// sdg: original diagonal (Cholesky-infinity test: a pivot below 1e-13 of it becomes 1e128).
 template <int N>
-__device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double& dinv0,
-                                         double& dinv1, const double* sdg, double* sdinv,
-                                         int l) {
-  dinv0 = 0.0;
-  dinv1 = 0.0;
+__device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
+                                         double& dinv0, double& dinv1, const double* sdg, int l) {
+  dinv0 = dinv1 = 1.0;
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    double dk = (s == 0) ? rowb<kl>(c0[k]) : rowb<kl>(c1[k]);
+    double dk = (s == 0) ? bcast_guarded<kl>(c0[k]) : bcast_guarded<kl>(c1[k]);
     if (!(dk > 1e-13 * sdg[k])) dk = 1e128;   // Cholesky-infinity (Wright; PCx)
     const double inv = recip(dk);
     const int ln = opaque(l);
@@ -457,44 +487,61 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
     const double t1 = (ln + kRow > k && ln + kRow < N) ? -c1[k] * inv : 0.0;
     static_for<k + 1, N>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      const double b = (s == 0) ? rowb<kl>(c0[i]) : rowb<kl>(c1[i]);
-      c1[i] = fma(b, t1, c1[i]);
-      if constexpr (k < kRow - 1) c0[i] = fma(b, t0, c0[i]);
+      if constexpr (s == 0) {
+        fmac_bcast<kl>(c1[i], c0[i], t1);
+        if constexpr (k < kRow - 1) fmac_bcast_self<kl>(c0[i], t0);
+      } else {
+        fmac_bcast_self<kl>(c1[i], t1);
+      }
     });
   });
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int ln = opaque(l);
-    c0[i] = (i > ln) ? c0[i] * dinv0 : c0[i];
-    c1[i] = (i > ln + kRow) ? c1[i] * dinv1 : c1[i];
-  }
-  sdinv[l] = dinv0;
-  if (l + kRow < N) sdinv[l + kRow] = dinv1;
 }
 
-// Solve K x = r with the factor above; slot values r0 (var l), r1 (var l+16) in, x out.
+// Solve K x = r with the factor above; r0 (var l), r1 (var l+16) in, x out.  Every lane of
+// the row is updated at every step (no lane masks): a lane whose value is already final saves
+// it at its own pivot step and may take garbage afterwards.
+//   forward   z = L^-1 r             a_j += (-z_k / D_k) * (L[j][k] D_k)
+//   backward  in D-scaled form       a_j = z_j - sum_{k>j} (L[k][j] D_j) x_k,  x_j = a_j / D_j
 template <int N>
 __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const double (&c1)[N],
-                                               double dinv0, double dinv1, const double* sdinv,
+                                               double dinv0, double dinv1,
                                                double& a0, double& a1, int l) {
-  static_for<0, N>([&](auto kc) {           // forward: L z = r
+  double z0 = 0.0, z1 = 0.0;                // z_j, saved at step j
+  static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    const double zs = ((s == 0) ? rowb<kl>(a0) : rowb<kl>(a1)) * sdinv[k];
     const int ln = opaque(l);
-    if constexpr (k < kRow - 1) a0 = (ln > k) ? fma(-c0[k], zs, a0) : a0;
-    a1 = (ln + kRow > k) ? fma(-c1[k], zs, a1) : a1;
+    double zv;
+    if constexpr (s == 0) {
+      zv = -a0 * dinv0;
+      z0 = (ln == kl) ? a0 : z0;
+    } else {
+      zv = -a1 * dinv1;
+      z1 = (ln == kl) ? a1 : z1;
+    }
+    fmac_bcast<kl, true>(a1, zv, c1[k]);
+    if constexpr (k < kRow - 1) fmac_bcast<kl>(a0, zv, c0[k]);
   });
-  a0 *= dinv0;                              // D w = z
-  a1 *= dinv1;
-  static_for<0, N>([&](auto kc) {           // backward: L^T x = w
+  a0 = z0;
+  a1 = z1;
+  double x0 = 0.0, x1 = 0.0;
+  static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    const double xk = (s == 0) ? rowb<kl>(a0) : rowb<kl>(a1);
     const int ln = opaque(l);
-    if constexpr (k >= 1) a0 = (ln < k) ? fma(-c0[k], xk, a0) : a0;
-    if constexpr (k > kRow) a1 = (ln + kRow < k) ? fma(-c1[k], xk, a1) : a1;
+    double nxv;
+    if constexpr (s == 0) {
+      nxv = -a0 * dinv0;
+      x0 = (ln == kl) ? nxv : x0;
+    } else {
+      nxv = -a1 * dinv1;
+      x1 = (ln == kl) ? nxv : x1;
+    }
+    if constexpr (k >= 1) fmac_bcast<kl, true>(a0, nxv, c0[k]);
+    if constexpr (k > kRow) fmac_bcast<kl, k < 1>(a1, nxv, c1[k]);
   });
+  a0 = -x0;
+  a1 = -x1;
 }
 
 template <class D>
@@ -520,7 +567,6 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
   double* sUv = B + D::I_UV;
   double* sVr = B + D::I_VR;
   double* sDr = B + D::I_DR;
-  double* sDinv = B + D::I_DINV;
   double* sDg = B + D::I_DG;
   double* sMask = B + D::I_MASK;
   double* sTau = B + D::I_TAU;
@@ -744,7 +790,7 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
-    ldl_rows<NY>(c0, c1, dinv0, dinv1, sDg, sDinv, l);
+    ldl_rows<NY>(c0, c1, dinv0, dinv1, sDg, l);
     wave_sync();
     STAMP_END(3);
 
@@ -768,7 +814,7 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
       dy1 = -rd1 + GTw(sVr, jj1, jk1, jc1);
       STAMP_END(4);
       STAMP_BEGIN();
-      ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, sDinv, dy0, dy1, l);
+      ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, dy0, dy1, l);
       sVy2[j0] = dy0;
       if (v1) sVy2[j1] = dy1;
       wave_sync();
