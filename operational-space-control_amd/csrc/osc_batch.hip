@@ -459,6 +459,40 @@ __device__ __forceinline__ double bcast_guarded(double v) {
   return r;
 }
 
+// a += bcast_K(src) * ma;  b += bcast_K(src) * mb  (one broadcast source, two slots).
+// NOP = true guards a source that a VALU instruction may have written just before.
+template <int K, bool NOP>
+__device__ __forceinline__ void fmac_bcast2(double& a, double& b, double src, double ma, double mb) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\t"
+                 "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+                 : "+v"(a), "+v"(b) : "v"(src), "v"(ma), "v"(mb), "n"(K));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+                 : "+v"(a), "+v"(b) : "v"(src), "v"(ma), "v"(mb), "n"(K));
+}
+
+// (a_i, b_i) += bcast_{i%16}(i < 16 ? x0 : x1) * (ma, mb)_i for i < N: the row group's
+// distributed vector x (x0 = x[lane], x1 = x[lane+16]) times lane-local columns.
+template <int N>
+__device__ __forceinline__ void rank1_rows(double (&a)[N], double (&b)[N], double x0, double x1,
+                                           double ma, double mb) {
+  static_for<0, N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    fmac_bcast2<i % kRow, i % kRow == 0>(a[i], b[i], i < kRow ? x0 : x1, ma, mb);
+  });
+}
+template <int N>
+__device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double x1,
+                                         const double (&ma)[N], const double (&mb)[N]) {
+  static_for<0, N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    fmac_bcast2<i % kRow, i % kRow == 0>(a, b, i < kRow ? x0 : x1, ma[i], mb[i]);
+  });
+}
+
 // LDL^T of an N x N symmetric matrix held one column per lane in two slots: lane l of a row
 // holds column l in c0 and column l+16 in c1.  Right-looking; at step k every lane j > k
 // applies  c_j[i] -= L[i][k] L[j][k] D_k  for i > k with the pivot column entry c_k[i]
@@ -744,26 +778,17 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
     // ---- Newton matrix K = Hr + G' D G (columns j0, j1 in registers) and rd = Hr y + g + G'lam
     double rd0 = g0 + GTw(sVr, j0, jk0, jc0), rd1 = g1 + GTw(sVr, jj1, jk1, jc1);
     double dg0 = hdg0, dg1 = hdg1;
-    if (!init) {
-#pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        rd0 = fma(c0[i], sVy[i], rd0);
-        rd1 = fma(c1[i], sVy[i], rd1);
-      }
-    }
+    if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
+    // U' diag(d) U: per torque row q, rank-1 update with u = U[q][.] broadcast from the lane
+    // holding it (DPP) -- no broadcast LDS reads in the loop.
 #pragma unroll 1
-    for (int q = 0; q < NU; ++q) {   // rolled: bounds the number of U loads in flight
+    for (int q = 0; q < NU; ++q) {
       const double du = sDr[2 * q] + sDr[2 * q + 1];
       const double u0 = sU[q * NY1P + j0], u1 = sU[q * NY1P + jj1];
       const double t0 = du * u0, t1 = du * u1;
       dg0 = fma(t0, u0, dg0);
       dg1 = fma(t1, u1, dg1);
-#pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        const double uqi = sU[q * NY1P + i];
-        c0[i] = fma(t0, uqi, c0[i]);
-        c1[i] = fma(t1, uqi, c1[i]);
-      }
+      rank1_rows<NY>(c0, c1, u0, u1, t0, t1);
     }
     if (jk0 >= 0) {
       double a, b, cc;
