@@ -167,6 +167,58 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
+// Compile-time lane masks.  A 16-bit pattern over the lanes of one row, replicated to all four
+// rows of the wave, is a 64-bit SGPR constant; selecting with it needs no per-lane compare.
+constexpr unsigned long long rows_mask(unsigned pattern16) {
+  return static_cast<unsigned long long>(pattern16 & 0xFFFFu) * 0x0001000100010001ull;
+}
+constexpr unsigned lanes_from(int lo, int hi) {   // lanes lo..hi of a row (empty if hi < lo)
+  unsigned m = 0;
+  for (int i = lo < 0 ? 0 : lo; i <= hi && i < 16; ++i) m |= 1u << i;
+  return m;
+}
+// The mask is materialized (s_mov) right at its use: left to itself hipcc hoists every
+// distinct mask of the unrolled loops into its own SGPR pair and spills them to VGPR lanes.
+template <unsigned long long MASK>
+__device__ __forceinline__ unsigned long long mask_here() {
+  static_assert((MASK >> 32) == (MASK & 0xFFFFFFFFull), "row-replicated masks only");
+  unsigned lo, hi;
+  asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %2" : "=s"(lo), "=s"(hi)
+               : "i"(static_cast<unsigned>(MASK & 0xFFFFFFFFull)));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+// MASK lanes take `set`, the others `clear` (v_cndmask_b32 x2 on an SGPR-pair mask).
+template <unsigned long long MASK>
+__device__ __forceinline__ double select_lanes(double set, double clear) {
+  if constexpr (MASK == 0ull) {
+    return clear;
+  } else if constexpr (MASK == ~0ull) {
+    return set;
+  } else {
+    int lo, hi;
+    asm("v_cndmask_b32_e64 %0, %2, %3, %6\n\tv_cndmask_b32_e64 %1, %4, %5, %6"
+        : "=&v"(lo), "=v"(hi)
+        : "v"(__double2loint(clear)), "v"(__double2loint(set)), "v"(__double2hiint(clear)),
+          "v"(__double2hiint(set)), "s"(mask_here<MASK>()));
+    return __hiloint2double(hi, lo);
+  }
+}
+// MASK lanes keep v, the others get +0.0.
+template <unsigned long long MASK>
+__device__ __forceinline__ double keep_lanes(double v) {
+  if constexpr (MASK == 0ull) {
+    return 0.0;
+  } else if constexpr (MASK == ~0ull) {
+    return v;
+  } else {
+    int lo, hi;
+    asm("v_cndmask_b32_e64 %0, 0, %2, %4\n\tv_cndmask_b32_e64 %1, 0, %3, %4"
+        : "=&v"(lo), "=v"(hi)
+        : "v"(__double2loint(v)), "v"(__double2hiint(v)), "s"(mask_here<MASK>()));
+    return __hiloint2double(hi, lo);
+  }
+}
+
 // Broadcast lane K of each 16-lane row to the whole row: v_mov_b64_dpp row_newbcast:K.
 template <int K>
 __device__ __forceinline__ double rowb(double v) {
@@ -249,6 +301,12 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // 1/d to full double precision: v_rcp_f64 + two Newton steps.
+// 1/d with one Newton step (v_rcp_f64 is good to ~2^-26; one step gives ~2^-52 in exact
+// arithmetic, a few ulp in practice) -- enough for pivots and barrier terms.
+__device__ __forceinline__ double recip1(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return fma(r, fma(-d, r, 1.0), r);
+}
 __device__ __forceinline__ double recip(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = fma(-d, r, 1.0);
@@ -487,10 +545,16 @@ __device__ __forceinline__ void rank1_rows(double (&a)[N], double (&b)[N], doubl
 template <int N>
 __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double x1,
                                          const double (&ma)[N], const double (&mb)[N]) {
+  double a2 = 0.0, b2 = 0.0;                // two chains: no back-to-back dependent f64 ops
   static_for<0, N>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    fmac_bcast2<i % kRow, i % kRow == 0>(a, b, i < kRow ? x0 : x1, ma[i], mb[i]);
+    if constexpr (i % 2 == 0)
+      fmac_bcast2<i % kRow, i % kRow == 0>(a, b, i < kRow ? x0 : x1, ma[i], mb[i]);
+    else
+      fmac_bcast2<i % kRow, false>(a2, b2, i < kRow ? x0 : x1, ma[i], mb[i]);
   });
+  a += a2;
+  b += b2;
 }
 
 // LDL^T of an N x N symmetric matrix held one column per lane in two slots: lane l of a row
@@ -510,15 +574,16 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
     constexpr int s = k / kRow, kl = k % kRow;
     double dk = (s == 0) ? bcast_guarded<kl>(c0[k]) : bcast_guarded<kl>(c1[k]);
     if (!(dk > 1e-13 * sdg[k])) dk = 1e128;   // Cholesky-infinity (Wright; PCx)
-    const double inv = recip(dk);
-    const int ln = opaque(l);
+    const double inv = recip1(dk);
+    constexpr unsigned long long kPiv = rows_mask(1u << kl);
     if constexpr (s == 0) {
-      dinv0 = (ln == kl) ? inv : dinv0;
+      dinv0 = select_lanes<kPiv>(inv, dinv0);
     } else {
-      dinv1 = (ln == kl) ? inv : dinv1;
+      dinv1 = select_lanes<kPiv>(inv, dinv1);
     }
-    const double t0 = (k < kRow - 1 && ln > k) ? -c0[k] * inv : 0.0;   // -L[lane][k]
-    const double t1 = (ln + kRow > k && ln + kRow < N) ? -c1[k] * inv : 0.0;
+    // -L[lane][k] for the lanes still to be eliminated (slot 0: lane > k; slot 1: lane+16 > k)
+    const double t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(-c0[k] * inv);
+    const double t1 = keep_lanes<rows_mask(lanes_from(k + 1 - kRow, N - 1 - kRow))>(-c1[k] * inv);
     static_for<k + 1, N>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (s == 0) {
@@ -544,14 +609,14 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    const int ln = opaque(l);
+    constexpr unsigned long long kPiv = rows_mask(1u << kl);
     double zv;
     if constexpr (s == 0) {
       zv = -a0 * dinv0;
-      z0 = (ln == kl) ? a0 : z0;
+      z0 = select_lanes<kPiv>(a0, z0);
     } else {
       zv = -a1 * dinv1;
-      z1 = (ln == kl) ? a1 : z1;
+      z1 = select_lanes<kPiv>(a1, z1);
     }
     fmac_bcast<kl, true>(a1, zv, c1[k]);
     if constexpr (k < kRow - 1) fmac_bcast<kl>(a0, zv, c0[k]);
@@ -562,14 +627,14 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    const int ln = opaque(l);
+    constexpr unsigned long long kPiv = rows_mask(1u << kl);
     double nxv;
     if constexpr (s == 0) {
       nxv = -a0 * dinv0;
-      x0 = (ln == kl) ? nxv : x0;
+      x0 = select_lanes<kPiv>(nxv, x0);
     } else {
       nxv = -a1 * dinv1;
-      x1 = (ln == kl) ? nxv : x1;
+      x1 = select_lanes<kPiv>(nxv, x1);
     }
     if constexpr (k >= 1) fmac_bcast<kl, true>(a0, nxv, c0[k]);
     if constexpr (k > kRow) fmac_bcast<kl, k < 1>(a1, nxv, c1[k]);
@@ -765,11 +830,13 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
         break;
       }
     }
+    double inv_s[NRL];                   // 1/s on active rows, 0 elsewhere (s = 1 at init)
 #pragma unroll
     for (int t = 0; t < NRL; ++t) {
       const int r = l + kRow * t;
+      inv_s[t] = act[t] ? (init ? 1.0 : recip(s[t])) : 0.0;
       sVr[r] = init ? 0.0 : (act[t] ? lam[t] : 0.0);
-      sDr[r] = act[t] ? (init ? 1.0 : lam[t] * recip(s[t])) : 0.0;
+      sDr[r] = init ? inv_s[t] : lam[t] * inv_s[t];
     }
     wave_sync();
 
@@ -824,15 +891,14 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
     double ds[NRL], dl[NRL], dsdl[NRL];
 #pragma unroll
     for (int t = 0; t < NRL; ++t) ds[t] = dl[t] = dsdl[t] = 0.0;
-    double dy0 = 0.0, dy1 = 0.0, sig_mu = 0.0, step = 1.0;
+    double dy0 = 0.0, dy1 = 0.0, sig_mu = 0.0, step = 1.0, a_aff = 1.0;
     const int npass = init ? 1 : 2;
     for (int pass = 0; pass < npass; ++pass) {
       STAMP_BEGIN();
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
         const double rc = fma(s[t], lam[t], dsdl[t]) - sig_mu;   // dsdl = sig_mu = 0 in pass 0
-        sVr[l + kRow * t] =
-            init ? (act[t] ? h[t] : 0.0) : (act[t] ? (rc - lam[t] * rp[t]) * recip(s[t]) : 0.0);
+        sVr[l + kRow * t] = init ? (act[t] ? h[t] : 0.0) : (rc - lam[t] * rp[t]) * inv_s[t];
       }
       wave_sync();
       dy0 = -rd0 + GTw(sVr, j0, jk0, jc0);
@@ -847,24 +913,24 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
       STAMP_BEGIN();
       uv_product(sVy2);
       wave_sync();
-      double ratio = 1.0;
+      // step to the boundary, division-free: 1 / max(1, max_r(-ds/s), max_r(-dl/lambda))
+      double rmax = 1.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
         const double rc = fma(s[t], lam[t], dsdl[t]) - sig_mu;
         const double gdy = Gv(sVy2, t);
         ds[t] = act[t] ? -rp[t] - gdy : 0.0;
-        dl[t] = act[t] ? -(rc + lam[t] * ds[t]) * recip(s[t]) : 0.0;
-        if (act[t]) {
-          if (ds[t] < 0.0) ratio = fmin(ratio, -s[t] * recip(ds[t]));
-          if (dl[t] < 0.0) ratio = fmin(ratio, -lam[t] * recip(dl[t]));
-        }
+        dl[t] = -(rc + lam[t] * ds[t]) * inv_s[t];
+        const double inv_l = (act[t] && !init) ? recip1(lam[t]) : 0.0;
+        rmax = fmax(rmax, fmax(-ds[t] * inv_s[t], -dl[t] * inv_l));
       }
-      step = row_min(ratio);
+      step = recip(row_max(rmax));
       if (pass == 0 && !init) {
         double ca = 0.0;
 #pragma unroll
         for (int t = 0; t < NRL; ++t)
           ca += act[t] ? (s[t] + step * ds[t]) * (lam[t] + step * dl[t]) : 0.0;
+        a_aff = step;
         const double mu_aff = row_sum(ca) / fmax(m_act, 1.0);
         const double q = mu_aff / fmax(mu, 1e-300);
         sig_mu = q * q * q * mu;
@@ -902,7 +968,12 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
         it_done = 0;
       }
     } else {
-      const double alpha = done ? 0.0 : fmin(1.0, 0.99 * step);
+      // fraction to the boundary: 0.99 early, closer to 1 as mu -> 0 or when the affine step was
+      // nearly full, never above 1 - 1e-5 (tools/ipm_model.py + tools/etatest.sh: -15% lockstep
+      // iterations vs a fixed 0.99; uncapped, a few envs stall at the boundary)
+      const double eta =
+          fmin(1.0 - 1e-5, fmax(0.99, fmax(1.0 - mu, 1.0 - 0.1 * (1.0 - a_aff))));
+      const double alpha = done ? 0.0 : fmin(1.0, eta * step);
       y0 = fma(alpha, dy0, y0);
       y1 = fma(alpha, dy1, y1);
 #pragma unroll

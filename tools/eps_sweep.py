@@ -1,0 +1,56 @@
+"""Diagnostic: interior-point stop threshold vs iterations, kernel time and accuracy against the
+golden oracle solutions (tests/golden).  Prints one JSON object per eps_mu."""
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from osc_amd.solver import OSCBatchSolver  # noqa: E402
+from osc_amd.synth import SEED_BASE, generate  # noqa: E402
+
+GOLD = sorted(glob.glob(os.path.join(REPO, "tests", "golden", "*.npz")))
+
+
+def kernel_ms(s, args, out, reps=10):
+    for _ in range(3):
+        s.solve_into(out, *args)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        s.solve_into(out, *args)
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+EPS = [float(a) for a in sys.argv[1:]] or [1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7]
+for eps in EPS:
+    row = {"eps_mu": eps}
+    err = 0.0
+    for path in GOLD:
+        g = np.load(path)
+        robot = str(g["robot"])
+        s = OSCBatchSolver(robot, eps_mu=eps)
+        r = s.solve(g["M"], g["C"], g["J"], g["b"], g["T"], g["mask"], want_x=True)
+        x = r.x.cpu().numpy()
+        for e in range(x.shape[0]):
+            ref = g["x"][e]
+            err = max(err, float(np.abs(x[e] - ref).max() / max(np.abs(ref).max(), 1.0)))
+    row["golden_max_norm_err"] = err
+    for robot, nenv in [("unitree_go2", 4096), ("unitree_go2", 65536), ("walter_sr", 4096)]:
+        s = OSCBatchSolver(robot, eps_mu=eps)
+        d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
+        args = s.prepare(**d)
+        out = s.alloc_outputs(nenv)
+        ms = kernel_ms(s, args, out)
+        it = out.iters.cpu().numpy()
+        st = out.status.cpu().numpy()
+        row[f"{robot}_{nenv}"] = {"ms": round(ms, 4), "mean_it": round(float(it.mean()), 2),
+                                  "wave_max_it": round(float(it.reshape(-1, 4).max(1).mean()), 2),
+                                  "ok": float((st == 0).mean())}
+    print(json.dumps(row), flush=True)

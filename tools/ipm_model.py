@@ -1,0 +1,200 @@
+"""Diagnostic (CPU): numpy model of osc_ipm_kernel's interior-point method on the reduced QP, for
+tuning the iteration strategy before touching the kernel.  Not a test and not product code.
+
+Reduced QP (as osc_setup_kernel builds it): y = (dv_a, z), dv_b and u affine in y,
+    min 1/2 y'Hr y + g'y   s.t.  G y + s = h, s >= 0
+rows: torque upper/lower interleaved (2q, 2q+1), then per contact k: 4 pyramid rows,
+-fz <= 0, fz <= 1e4 (masked contacts: no rows, z pinned to 0).
+
+Usage: python tools/ipm_model.py [robot] [nenv] [variant ...]
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import numpy as np  # noqa: E402
+import scipy.linalg as sla  # noqa: E402
+from osc_amd.synth import SEED_BASE, generate  # noqa: E402
+from osc_qp import BIG_NUMBER, build_qp, contact_jacobian, load_model  # noqa: E402
+
+
+def reduce_qp(model, M, C, J, b, T, mask):
+    qp = build_qp(model, M, C, J, b, T, mask)
+    nv, nu, nc = model.nv, model.nu, model.nc
+    nz, NB = 3 * nc, nv - nu
+    NY = nu + nz
+    n = model.n
+    Jc = contact_jacobian(model, J)
+    pinned = np.repeat(np.asarray(mask) == 0, 3)
+    Jcm = Jc * (~pinned)[None, :]
+    Mbb_inv = np.linalg.inv(M[:NB, :NB])
+    # dv_b = Xy y + x0
+    Xy = np.hstack([-Mbb_inv @ M[:NB, NB:], Mbb_inv @ Jcm[:NB]])
+    x0 = -Mbb_inv @ C[:NB]
+    # u = M[NB:, :NB] dv_b + M[NB:, NB:] dv_a + C_a - Jc_a z
+    Uy = M[NB:, :NB] @ Xy + np.hstack([M[NB:, NB:], -Jcm[NB:]])
+    u0 = M[NB:, :NB] @ x0 + C[NB:]
+    P = np.zeros((n, NY))
+    p0 = np.zeros(n)
+    P[:NB] = Xy
+    p0[:NB] = x0
+    P[NB:nv, :nu] = np.eye(nu)
+    P[nv:nv + nu] = Uy
+    p0[nv:nv + nu] = u0
+    P[nv + nu:, nu:] = np.eye(nz)
+    Hr = P.T @ qp.H @ P
+    g = P.T @ (qp.H @ p0 + qp.f)
+    rows, hs = [], []
+    for q in range(nu):
+        rows.append(Uy[q]); hs.append(model.u_ub[q] - u0[q])
+        rows.append(-Uy[q]); hs.append(u0[q] - model.u_lb[q])
+    for k in range(nc):
+        if mask[k] == 0:
+            continue
+        zc = nu + 3 * k
+        for sx, sy in ((1, 1), (-1, 1), (1, -1), (-1, -1)):
+            r = np.zeros(NY); r[zc] = sx; r[zc + 1] = sy; r[zc + 2] = -model.mu
+            rows.append(r); hs.append(0.0)
+        r = np.zeros(NY); r[zc + 2] = -1.0; rows.append(r); hs.append(0.0)
+        r = np.zeros(NY); r[zc + 2] = 1.0; rows.append(r); hs.append(BIG_NUMBER * mask[k])
+    return Hr, g, np.array(rows), np.array(hs), P, p0
+
+
+def ldl_factor(K):
+    """The kernel's LDL^T: right-looking, Cholesky-infinity guard (pivot <= 1e-13 * original
+    diagonal -> 1e128), as ldl_rows in osc_batch.hip."""
+    A = K.copy()
+    n = len(A)
+    dg = np.diag(K).copy()
+    L = np.eye(n)
+    d = np.zeros(n)
+    for k in range(n):
+        dk = A[k, k]
+        if not dk > 1e-13 * dg[k]:
+            dk = 1e128
+        d[k] = dk
+        col = A[k + 1:, k] / dk
+        L[k + 1:, k] = col
+        A[k + 1:, k + 1:] -= np.outer(col, A[k, k + 1:])
+    return L, d
+
+
+def ldl_solve(F, r):
+    L, d = F
+    z = sla.solve_triangular(L, r, lower=True, unit_diagonal=True)
+    return sla.solve_triangular(L.T, z / d, lower=False, unit_diagonal=True)
+
+
+def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
+    m = len(h)
+    K0 = Hr + G.T @ G
+    y = np.linalg.solve(K0, -g + G.T @ h)
+    zr = G @ y - h
+    if "mehrotra_init" in variant:
+        s, lam = -zr.copy(), zr.copy()
+        ds_ = max(-1.5 * s.min(), 0.0); dl_ = max(-1.5 * lam.min(), 0.0)
+        s += ds_; lam += dl_
+        sl = s @ lam
+        s += 0.5 * sl / lam.sum(); lam += 0.5 * sl / s.sum()
+    elif any(v.startswith("shift") for v in variant):
+        c = [float(v[5:]) for v in variant if v.startswith("shift")][0]
+        ap, ad = -(-zr).min(), -zr.min()
+        s = -zr + (c + ap if ap >= 0 else 0.0)
+        lam = zr + (c + ad if ad >= 0 else 0.0)
+    else:
+        ap, ad = (-zr).min(), zr.min()          # kernel: shift by 1 + max(-s), 1 + max(-lambda)
+        ap, ad = -ap, -ad
+        s = -zr + (1.0 + ap if ap >= 0 else 0.0)
+        lam = zr + (1.0 + ad if ad >= 0 else 0.0)
+    eta = 0.99
+    for it in range(max_iter + 1):
+        rp = G @ y + s - h
+        rd = Hr @ y + g + G.T @ lam
+        mu = s @ lam / m
+        if mu <= eps_mu:
+            return y, it, True
+        if it >= max_iter:
+            return y, it, False
+        D = lam / s
+        K = Hr + G.T @ (D[:, None] * G)
+        Kf = ldl_factor(K)
+
+        def direction(rc):
+            w = (rc - lam * rp) / s
+            dy = ldl_solve(Kf, -rd + G.T @ w)
+            ds = -rp - G @ dy
+            dl = -(rc + lam * ds) / s
+            return dy, ds, dl
+
+        def max_step(ds, dl):
+            a = 1.0
+            neg = ds < 0
+            if neg.any():
+                a = min(a, (-s[neg] / ds[neg]).min())
+            neg = dl < 0
+            if neg.any():
+                a = min(a, (-lam[neg] / dl[neg]).min())
+            return a
+
+        dy, ds, dl = direction(s * lam)
+        a_aff = max_step(ds, dl)
+        mu_aff = (s + a_aff * ds) @ (lam + a_aff * dl) / m
+        sig = (mu_aff / mu) ** 3
+        rc = s * lam + ds * dl - sig * mu
+        dy, ds, dl = direction(rc)
+        a = max_step(ds, dl)
+        if "gondzio" in variant:
+            # one centrality corrector (Gondzio 1996): push complementarity products into a box
+            at = min(1.0, 1.5 * a + 0.1)
+            st, lt = s + at * ds, lam + at * dl
+            v = st * lt
+            tgt = sig * mu
+            lo, hi = 0.1 * tgt, 10.0 * tgt
+            corr = np.where(v < lo, lo - v, np.where(v > hi, np.maximum(hi - v, -hi), 0.0))
+            dy2, ds2, dl2 = direction(rc - corr)
+            a2 = max_step(ds2, dl2)
+            if a2 >= 1.01 * a:
+                dy, ds, dl, a = dy2, ds2, dl2, a2
+        if "eta" in variant:
+            eta = max(0.99, 1.0 - mu)
+        for v in variant:
+            if v.startswith("etafix"):
+                eta = float(v[6:])
+            if v.startswith("etak"):        # eta = max(0.99, 1 - k mu)
+                eta = max(0.99, 1.0 - float(v[4:]) * mu)
+            if v.startswith("etaa"):        # eta = max(0.99, 1 - a_aff-based)  (PCx-like)
+                eta = max(0.99, 1.0 - (1.0 - a_aff) * float(v[4:]))
+            if v.startswith("etam"):        # eta = max(0.99, 1 - mu, 1 - c (1 - a_aff))
+                eta = max(0.99, 1.0 - mu, 1.0 - (1.0 - a_aff) * float(v[4:]))
+            if v.startswith("cap"):         # eta <= 1 - c
+                eta = min(eta, 1.0 - float(v[3:]))
+        alpha = min(1.0, eta * a)
+        y, s, lam = y + alpha * dy, s + alpha * ds, lam + alpha * dl
+    return y, max_iter, False
+
+
+def main():
+    robot = sys.argv[1] if len(sys.argv) > 1 else "unitree_go2"
+    nenv = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    variants = [tuple(v.split("+")) if v != "base" else () for v in (sys.argv[3:] or ["base"])]
+    model = load_model(robot)
+    d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
+    probs = [reduce_qp(model, *(d[k][e] for k in ("M", "C", "J", "b", "T", "mask")))
+             for e in range(nenv)]
+    ref = [ipm(*p[:4], eps_mu=1e-12, max_iter=80)[0] for p in probs]
+    for v in variants:
+        its, errs = [], []
+        for p, yr in zip(probs, ref):
+            y, it, ok = ipm(*p[:4], variant=v)
+            its.append(it)
+            errs.append(np.abs(y - yr).max() / max(np.abs(yr).max(), 1.0))
+        its = np.array(its)
+        print(f"{'+'.join(v) or 'base':24s} fail {int((its >= 40).sum())} mean_it {its.mean():6.2f}  wave4_max "
+              f"{its.reshape(-1, 4).max(1).mean():6.2f}  max_it {its.max():3d}  "
+              f"max_err {max(errs):.2e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -18,7 +18,7 @@ from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble K", "LDL^T", "rhs (2 passes)",
          "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update"]
 for robot in ["unitree_go2", "walter_sr"]:
-    nenv = 16384
+    nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     s = OSCBatchSolver(robot)
     d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
     args = s.prepare(**d)
