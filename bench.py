@@ -28,7 +28,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from osc_amd.robots import bytes_per_solve, dims  # noqa: E402
-from osc_amd.synth import SEED_BASE, generate, random_walk  # noqa: E402
+from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
 METRIC = "OSC control steps/sec (batched envs), Go2 18-DoF, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -44,30 +44,33 @@ def algorithmic_flops(robot: str, iters: float) -> float:
     return f0 + iters * fit
 
 
-def cpu_baseline(robot: str, seconds: float) -> dict:
+def cpu_baseline(robot: str, seconds: float, cores: int) -> dict:
     """Reference CPU path restated (oracle/osc_ref_port.c: CasADi-equivalent assembly + OSQP
-    0.6.3 ADMM, warm start) on ONE host core: a single environment ticking through a 1 %
-    random walk of its inputs, no 500 Hz sleep."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from ref_port import RefPort  # checker / baseline only
-    rng = np.random.default_rng(SEED_BASE)
-    d = generate(robot, 1, SEED_BASE + 1, "standing", "ones")
-    ticks = [d]
-    for _ in range(63):
-        ticks.append(random_walk(ticks[-1], rng))
-    inputs = [[t[k][0] for k in ("M", "C", "J", "b", "T", "mask")] for t in ticks]
-    port = RefPort(robot)
-    for a in inputs[:4]:
-        port.step(*a)
-    n, iters, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        _, it = port.step(*inputs[n % len(inputs)])
-        iters += it
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{robot} single env, {n} warm-started ticks over a 64-tick 1% random walk "
-                      f"in {dt:.1f} s on 1 host core (mean {iters / max(n, 1):.0f} ADMM iters/tick)"}
+    0.6.3 ADMM, warm start): each worker process ticks ONE environment through a 1 % random
+    walk of its inputs with no 500 Hz sleep (oracle/ref_port.py timed_ticks).  Run once on
+    1 core, then `cores` independent workers at once."""
+    import subprocess
+    worker = [sys.executable, os.path.join(REPO, "oracle", "ref_port.py"), "--robot", robot,
+              "--seconds", str(seconds)]
+
+    def run(n):
+        procs = [subprocess.Popen(worker + ["--seed", str(k)], stdout=subprocess.PIPE, text=True)
+                 for k in range(n)]
+        res = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+        if any(p.returncode != 0 for p in procs):
+            raise RuntimeError("cpu baseline worker failed")
+        return res
+
+    one = run(1)[0]
+    many = run(cores)
+    rate1 = one["ticks"] / one["seconds"]
+    rate = sum(r["ticks"] / r["seconds"] for r in many)
+    iters = sum(r["admm_iters"] for r in many) / max(sum(r["ticks"] for r in many), 1)
+    return {"value": rate, "unit": "solves/s", "cores": cores, "kind": "port",
+            "single_core_value": rate1,
+            "sample": f"{robot}: {cores} worker processes x 1 env each, warm-started ticks over a "
+                      f"64-tick 1% random walk for {seconds:.0f} s (mean {iters:.0f} ADMM "
+                      f"iters/tick); single core alone {rate1:.0f} solves/s"}
 
 
 def main() -> None:
@@ -79,7 +82,9 @@ def main() -> None:
     ap.add_argument("--nenv-per-gpu", type=int, default=4096)
     ap.add_argument("--scenario", default="standing", choices=["standing", "tumbling"])
     ap.add_argument("--mask", default="ones", choices=["ones", "bernoulli"])
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1),
+                    help="CPU baseline worker processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
@@ -109,26 +114,33 @@ def main() -> None:
         solver.solve_into(out, *inputs)
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # Each step = osc_batch_assemble (setup kernel) + osc_batch_solve_assembled (interior-point
+    # kernel), the two halves of osc_batch_solve, with HIP events on the launch stream around
+    # each kernel.
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    mask = inputs[5]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        solver.solve_into(out, *inputs)
+        solver.assemble_into(out, *inputs)
         ev[k][1].record(stream)
+        solver.solve_assembled_into(out, mask)
+        ev[k][2].record(stream)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    kernel_ms = setup_ms + ipm_ms
 
     st = out.status.cpu().numpy()
     mean_iters = float(out.iters.double().mean().item())
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kernel_ms, setup_ms, ipm_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, kernel_ms, setup_ms, ipm_ms = (float(v) for v in t)
         c = torch.tensor([float((st == 0).sum()), float(st.size)], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(c)
         converged = float(c[0] / c[1])
@@ -167,14 +179,17 @@ def main() -> None:
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_solve": bps, "kernel_ms": kernel_ms},
+                         "kernel": "osc_setup_kernel + osc_ipm_kernel (one batched solve)",
+                         "bytes_per_solve": bps, "kernel_ms": kernel_ms,
+                         "kernel_ms_split": {"osc_setup_kernel": setup_ms,
+                                             "osc_ipm_kernel": ipm_ms}},
             "roofline_fp64": {"achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": tflops / FP64_PEAK_TFLOPS,
                               "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
             "converged_frac": converged,
         }
         if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args.robot, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.robot, args.cpu_seconds, args.cpu_cores)
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -121,9 +121,7 @@ struct Dims {
   static constexpr int I_UV = I_VY2 + even(NY);        // U_y v for the torque rows
   static constexpr int I_VR = I_UV + even(NU);         // a row-space vector
   static constexpr int I_DR = I_VR + NRL * kRow;       // lambda / s
-  static constexpr int I_DINV = I_DR + NRL * kRow;     // 1 / D of the LDL^T factor
-  static constexpr int I_DG = I_DINV + even(NY);       // original diagonal of K
-  static constexpr int I_MASK = I_DG + even(NY);
+  static constexpr int I_MASK = I_DR + NRL * kRow;
   static constexpr int I_TAU = I_MASK + even(NC);
   static constexpr int I_XB = I_TAU + even(NU);
   static constexpr int IL = I_XB + even(NB);
@@ -159,14 +157,6 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ---- lane primitives ----------------------------------------------------------------------
-// An empty asm that "modifies" x: comparisons against the lane id made right after it cannot
-// be hoisted out of loops (hipcc otherwise precomputes one 64-bit lane mask per unrolled step,
-// hundreds of SGPRs, and spills them).
-__device__ __forceinline__ int opaque(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
 // Compile-time lane masks.  A 16-bit pattern over the lanes of one row, replicated to all four
 // rows of the wave, is a 64-bit SGPR constant; selecting with it needs no per-lane compare.
 constexpr unsigned long long rows_mask(unsigned pattern16) {
@@ -300,13 +290,13 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// 1/d to full double precision: v_rcp_f64 + two Newton steps.
 // 1/d with one Newton step (v_rcp_f64 is good to ~2^-26; one step gives ~2^-52 in exact
 // arithmetic, a few ulp in practice) -- enough for pivots and barrier terms.
 __device__ __forceinline__ double recip1(double d) {
   const double r = __builtin_amdgcn_rcp(d);
   return fma(r, fma(-d, r, 1.0), r);
 }
+// 1/d to full double precision: v_rcp_f64 + two Newton steps.
 __device__ __forceinline__ double recip(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = fma(-d, r, 1.0);
@@ -567,13 +557,16 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // sdg: original diagonal (Cholesky-infinity test: a pivot below 1e-13 of it becomes 1e128).
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
-                                         double& dinv0, double& dinv1, const double* sdg, int l) {
+                                         double& dinv0, double& dinv1, double thr0, double thr1) {
   dinv0 = dinv1 = 1.0;
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    double dk = (s == 0) ? bcast_guarded<kl>(c0[k]) : bcast_guarded<kl>(c1[k]);
-    if (!(dk > 1e-13 * sdg[k])) dk = 1e128;   // Cholesky-infinity (Wright; PCx)
+    // Cholesky-infinity (Wright; PCx): a pivot not above 1e-13 x its column's original diagonal
+    // (thr, lane-local) becomes 1e128.  Every lane tests its own slot-s entry k; only the pivot
+    // lane's result -- the true diagonal -- is broadcast, so no LDS round trip per step.
+    const double own = (s == 0) ? c0[k] : c1[k];
+    const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
     const double inv = recip1(dk);
     constexpr unsigned long long kPiv = rows_mask(1u << kl);
     if constexpr (s == 0) {
@@ -658,7 +651,13 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
   const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
 
   double* B = sm + grp * D::IL;
-  const double* gHr = ws + static_cast<size_t>(env) * D::WS + D::W_HR;   // global, L2-resident
+  // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
+  // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
+  // (scratch loads share vmcnt) used to serialise the whole prefetch.
+  const double* __restrict__ wsw =
+      ws + static_cast<size_t>(blockIdx.x) * kEnvPerWave * D::WS + D::W_HR;   // L2-resident
+  const unsigned lane_off = static_cast<unsigned>(env - static_cast<int>(blockIdx.x) * kEnvPerWave) *
+                            static_cast<unsigned>(D::WS);
   double* sG = B + D::I_G;
   double* sU = B + D::I_U;
   double* sVy = B + D::I_VY;
@@ -666,7 +665,6 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
   double* sUv = B + D::I_UV;
   double* sVr = B + D::I_VR;
   double* sDr = B + D::I_DR;
-  double* sDg = B + D::I_DG;
   double* sMask = B + D::I_MASK;
   double* sTau = B + D::I_TAU;
   double* sXb = B + D::I_XB;
@@ -774,13 +772,20 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
   // Hr columns j0, j1 (and their diagonal entries) -> registers; re-issued at the end of every
   // iteration so the loads fly while the step is applied and the next residuals are formed.
   auto load_hr = [&]() {
+    // column bases formed here, every time (hidden from loop-invariant hoisting): kept live
+    // across the loop they get spilled, and spill reloads wait on vmcnt(0)
+    unsigned off = lane_off;
+    asm volatile("" : "+v"(off));
+    const double* p0 = wsw + off + j0;
+    const double* p1 = wsw + off + jj1;
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
-      c0[i] = gHr[i * NY + j0];
-      c1[i] = gHr[i * NY + jj1];
+      c0[i] = p0[i * NY];
+      c1[i] = p1[i * NY];
     }
   };
-  const double hdg0 = gHr[j0 * NY + j0], hdg1 = gHr[jj1 * NY + jj1];
+  const double hdg0 = wsw[lane_off + static_cast<unsigned>(j0 * NY + j0)];
+  const double hdg1 = wsw[lane_off + static_cast<unsigned>(jj1 * NY + jj1)];
   load_hr();
   const double g0 = sG[j0], g1 = sG[jj1];
   double y0 = 0.0, y1 = 0.0;
@@ -848,10 +853,15 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
     if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
     // U' diag(d) U: per torque row q, rank-1 update with u = U[q][.] broadcast from the lane
     // holding it (DPP) -- no broadcast LDS reads in the loop.
+    // rolled (I-cache, registers); the next row's three LDS reads are issued one trip ahead
+    double du_n = sDr[0] + sDr[1], u0_n = sU[j0], u1_n = sU[jj1];
 #pragma unroll 1
     for (int q = 0; q < NU; ++q) {
-      const double du = sDr[2 * q] + sDr[2 * q + 1];
-      const double u0 = sU[q * NY1P + j0], u1 = sU[q * NY1P + jj1];
+      const double du = du_n, u0 = u0_n, u1 = u1_n;
+      const int qn = (q + 1 < NU) ? q + 1 : q;
+      du_n = sDr[2 * qn] + sDr[2 * qn + 1];
+      u0_n = sU[qn * NY1P + j0];
+      u1_n = sU[qn * NY1P + jj1];
       const double t0 = du * u0, t1 = du * u1;
       dg0 = fma(t0, u0, dg0);
       dg1 = fma(t1, u1, dg1);
@@ -877,12 +887,10 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
         c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
       }
     }
-    sDg[j0] = dg0;
-    if (v1) sDg[j1] = dg1;
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
-    ldl_rows<NY>(c0, c1, dinv0, dinv1, sDg, l);
+    ldl_rows<NY>(c0, c1, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
     wave_sync();
     STAMP_END(3);
 
@@ -1146,36 +1154,41 @@ extern "C" int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t*
 
 namespace {
 
+enum Stage : unsigned { kAssemble = 1u, kInteriorPoint = 2u, kBoth = 3u };
+
 template <class D>
-int launch_t(const osc_model* model, int32_t nenv, const double* M, const double* C,
-             const double* J, const double* b, const double* T, const double* mask, double* tau,
-             double* x, int32_t* status, int32_t* iters, double* ws, hipStream_t s,
-             bool setup_only) {
-  hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
-                     model->dparams, nenv, M, C, J, b, T, mask, ws);
-  if (!setup_only) {
+void launch_t(const osc_model* model, int32_t nenv, const double* M, const double* C,
+              const double* J, const double* b, const double* T, const double* mask, double* tau,
+              double* x, int32_t* status, int32_t* iters, double* ws, hipStream_t s,
+              unsigned stages) {
+  if (stages & kAssemble)
+    hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
+                       model->dparams, nenv, M, C, J, b, T, mask, ws);
+  if (stages & kInteriorPoint) {
     const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
     hipLaunchKernelGGL(osc_ipm_kernel<D>, dim3(nb), dim3(kWave), 0, s, model->dparams, nenv,
                        mask, ws, tau, x, status, iters);
   }
-  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
 }
+
+bool misaligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
 
 int launch(const osc_model* model, int32_t nenv, const double* M, const double* C, const double* J,
            const double* b, const double* T, const double* contact_mask, double* tau, double* x,
            int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes,
-           void* stream, bool setup_only) {
+           void* stream, unsigned stages) {
   if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
   if (nenv == 0) return OSC_OK;
-  if (!M || !C || !J || !b || !T || !contact_mask || (!tau && !setup_only))
-    return OSC_ERR_INVALID_ARGUMENT;
-  // 16-byte alignment is required by the vectorised staging loads.
-  const uintptr_t align = reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(C) |
-                          reinterpret_cast<uintptr_t>(J) | reinterpret_cast<uintptr_t>(b) |
-                          reinterpret_cast<uintptr_t>(T) |
-                          reinterpret_cast<uintptr_t>(contact_mask) |
-                          reinterpret_cast<uintptr_t>(workspace);
-  if (align & 15u) return OSC_ERR_INVALID_ARGUMENT;
+  if (!contact_mask || misaligned16(contact_mask)) return OSC_ERR_INVALID_ARGUMENT;
+  if ((stages & kAssemble) && (!M || !C || !J || !b || !T || misaligned16(M) ||
+                               misaligned16(C) || misaligned16(J) || misaligned16(b) ||
+                               misaligned16(T)))
+    return OSC_ERR_INVALID_ARGUMENT;   // 16-byte alignment: vectorised staging loads
+  if ((stages & kInteriorPoint) && !tau) return OSC_ERR_INVALID_ARGUMENT;
+  // A split call hands the reduced QP over in the caller's workspace; only the fused call may
+  // take scratch of its own.
+  if (stages != kBoth && !workspace) return OSC_ERR_INVALID_ARGUMENT;
+  if (misaligned16(workspace)) return OSC_ERR_INVALID_ARGUMENT;
   size_t need = 0;
   osc_workspace_bytes(model, nenv, &need);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1187,19 +1200,19 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
   } else if (workspace_bytes < need) {
     return OSC_ERR_INVALID_ARGUMENT;
   }
-  int rc;
+  int rc = OSC_OK;
   switch (model->kid) {
     case K_GO2:
-      rc = launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s,
-                         setup_only);
+      launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s, stages);
       break;
     case K_WALTER:
-      rc = launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws,
-                            s, setup_only);
+      launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s,
+                       stages);
       break;
     default:
       rc = OSC_ERR_UNSUPPORTED_DIMS;
   }
+  if (rc == OSC_OK && hipGetLastError() != hipSuccess) rc = OSC_ERR_DEVICE;
   if (owned) (void)hipFreeAsync(ws, s);
   return rc;
 }
@@ -1212,7 +1225,24 @@ extern "C" int osc_batch_solve(const osc_model* model, int32_t nenv, const doubl
                                int32_t* status, int32_t* iters, void* workspace,
                                size_t workspace_bytes, void* stream) {
   return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
-                workspace_bytes, stream, false);
+                workspace_bytes, stream, kBoth);
+}
+
+extern "C" int osc_batch_assemble(const osc_model* model, int32_t nenv, const double* M,
+                                  const double* C, const double* J, const double* b,
+                                  const double* T, const double* contact_mask, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
+                workspace, workspace_bytes, stream, kAssemble);
+}
+
+extern "C" int osc_batch_solve_assembled(const osc_model* model, int32_t nenv,
+                                         const double* contact_mask, double* tau, double* x,
+                                         int32_t* status, int32_t* iters, const void* workspace,
+                                         size_t workspace_bytes, void* stream) {
+  return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, nullptr, contact_mask, tau, x,
+                status, iters, const_cast<void*>(workspace), workspace_bytes, stream,
+                kInteriorPoint);
 }
 
 #ifdef OSC_STAMPS
@@ -1223,22 +1253,3 @@ extern "C" int osc_debug_stamps(unsigned long long* host, int nblocks) {
                              nblocks) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
 }
 #endif
-
-// Test hook, not part of include/osc_batch.h: run only the setup kernel and leave the reduced
-// QP [Hr (NY x NY) | g (NY, padded even) | U (NU x NY1P) | X (NB x NY1P)] of every env in
-// `dbg` (device pointer, osc_debug_dump_size() doubles per env).  tests/test_gpu_stages.py.
-extern "C" int osc_debug_dump_size(const osc_model* model) {
-  if (!model) return -1;
-  return ws_doubles(model->kid);
-}
-
-extern "C" int osc_debug_reduced_qp(const osc_model* model, int32_t nenv, const double* M,
-                                    const double* C, const double* J, const double* b,
-                                    const double* T, const double* contact_mask, double* dbg,
-                                    void* stream) {
-  if (!dbg) return OSC_ERR_INVALID_ARGUMENT;
-  size_t need = 0;
-  if (osc_workspace_bytes(model, nenv, &need) != OSC_OK) return OSC_ERR_INVALID_ARGUMENT;
-  return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
-                dbg, need, stream, true);
-}

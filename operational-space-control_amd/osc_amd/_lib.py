@@ -21,7 +21,8 @@ SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL = 0, 1, 2
 
 EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
                     "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
-                    "osc_batch_solve", "osc_status_string", "osc_abi_version")
+                    "osc_batch_solve", "osc_batch_assemble", "osc_batch_solve_assembled",
+                    "osc_status_string", "osc_abi_version")
 
 
 class OscModelDesc(ctypes.Structure):
@@ -77,11 +78,10 @@ def lib() -> ctypes.CDLL:
     L.osc_status_string.restype = ctypes.c_char_p
     L.osc_abi_version.argtypes = []
     L.osc_abi_version.restype = ctypes.c_int
-    # test hooks (not in the public header)
-    L.osc_debug_dump_size.argtypes = [vp]
-    L.osc_debug_dump_size.restype = ctypes.c_int
-    L.osc_debug_reduced_qp.argtypes = [vp, i32] + [vp] * 8
-    L.osc_debug_reduced_qp.restype = ctypes.c_int
+    L.osc_batch_assemble.argtypes = [vp, i32] + [vp] * 6 + [vp, ctypes.c_size_t, vp]
+    L.osc_batch_assemble.restype = ctypes.c_int
+    L.osc_batch_solve_assembled.argtypes = [vp, i32] + [vp] * 5 + [vp, ctypes.c_size_t, vp]
+    L.osc_batch_solve_assembled.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -105,6 +105,33 @@ class OSCBatchSolver:
             raise _lib.OSCError("osc_batch_solve", rc)
         return out
 
+    def assemble_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None) -> SolveResult:
+        """First half of solve_into: every env's reduced QP into out.workspace."""
+        nenv = out.tau.shape[0]
+        s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        rc = _lib.lib().osc_batch_assemble(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
+                                           ptr(mask), ptr(out.workspace),
+                                           ctypes.c_size_t(out.workspace.numel() * 8),
+                                           ctypes.c_void_p(s))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_assemble", rc)
+        return out
+
+    def solve_assembled_into(self, out: SolveResult, mask, stream=None) -> SolveResult:
+        """Second half of solve_into: interior-point solve of the assembled workspace."""
+        nenv = out.tau.shape[0]
+        s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = _lib.lib().osc_batch_solve_assembled(self._h, nenv, ptr(mask), ptr(out.tau),
+                                                  ptr(out.x), ptr(out.status), ptr(out.iters),
+                                                  ptr(out.workspace),
+                                                  ctypes.c_size_t(out.workspace.numel() * 8),
+                                                  ctypes.c_void_p(s))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_solve_assembled", rc)
+        return out
+
     def prepare(self, M, C, J, b, T, mask):
         d = self.dims
         nenv = int(M.shape[0])

@@ -65,3 +65,39 @@ class RefPort:
             lib().osc_cpu_destroy(self._h)
         except Exception:
             pass
+
+
+def timed_ticks(robot: str, seconds: float, seed: int) -> dict:
+    """bench.py cpu_baseline worker: ONE environment ticking through a 64-tick 1 % random walk
+    of its inputs (warm-started, no 500 Hz sleep) for `seconds` on the calling core."""
+    import sys
+    import time
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "operational-space-control_amd"))
+    from osc_amd.synth import SEED_BASE, generate, random_walk
+    rng = np.random.default_rng(SEED_BASE + seed)
+    d = generate(robot, 1, SEED_BASE + 1 + seed, "standing", "ones")
+    ticks = [d]
+    for _ in range(63):
+        ticks.append(random_walk(ticks[-1], rng))
+    inputs = [[t[k][0] for k in ("M", "C", "J", "b", "T", "mask")] for t in ticks]
+    port = RefPort(robot)
+    for a in inputs[:4]:
+        port.step(*a)
+    n, iters, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, it = port.step(*inputs[n % len(inputs)])
+        iters += it
+        n += 1
+    return {"ticks": n, "admm_iters": iters, "seconds": time.perf_counter() - t0}
+
+
+if __name__ == "__main__":
+    import argparse
+    import json
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--robot", default="unitree_go2")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    print(json.dumps(timed_ticks(a.robot, a.seconds, a.seed)), flush=True)

@@ -70,6 +70,8 @@ def test_error_codes():
     d.z_ub[0] = 5.0                             # finite fx bound: not in the reference QP
     assert L.osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 1
     assert L.osc_batch_solve(None, 1, *([None] * 10), None, 0, None) == 1
+    assert L.osc_batch_assemble(None, 1, *([None] * 6), None, 0, None) == 1
+    assert L.osc_batch_solve_assembled(None, 1, *([None] * 5), None, 0, None) == 1
     assert L.osc_model_destroy(None) == 1
 
 

@@ -1,4 +1,4 @@
-"""GPU stage parity: the reduced QP the kernel builds (phases A-D) is checked against the
+"""GPU stage parity: the reduced QP osc_batch_assemble builds (setup kernel, phases A-D) is checked against the
 oracle's full QP (oracle/osc_qp.py) through properties that do not depend on how the
 reduction is computed:
   * x(y) = (dv_b = X[y;1], dv_a = y_u, u = U[y;1], z = y_z) satisfies the dynamics equality
@@ -34,17 +34,19 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     inp = generate(robot, nenv, SEED_BASE + 31, "tumbling", mask_mode)
     args = s.prepare(**inp)
     L = _lib.lib()
-    sz = L.osc_debug_dump_size(s._h)
+    nbytes = ctypes.c_size_t()
+    assert L.osc_workspace_bytes(s._h, nenv, ctypes.byref(nbytes)) == 0
+    sz = nbytes.value // 8 // nenv
     ev = lambda a: (a + 1) // 2 * 2
     ny1p = ev(ny + 1)
     o_g, o_u = 0, ev(ny)
     o_hr = o_u + nu * ny1p
     o_x = o_hr + ev(ny * ny)
-    assert sz == o_x + nb * ny1p
+    assert sz == o_x + nb * ny1p                # layout documented in include/osc_batch.h
     dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
-    rc = L.osc_debug_reduced_qp(s._h, nenv, *[p(a) for a in args], p(dbg),
-                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    rc = L.osc_batch_assemble(s._h, nenv, *[p(a) for a in args], p(dbg), nbytes,
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     assert rc == 0
     torch.cuda.synchronize()
     D = dbg.cpu().numpy()
@@ -79,3 +81,19 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
             objs.append((full, red, abs(full) + 0.5 * np.abs(x) @ np.abs(qp.H) @ np.abs(x)))
         for (f0, r0, s0), (f1, r1, s1) in zip(objs, objs[1:]):
             assert abs((f1 - f0) - (r1 - r0)) <= 1e-11 * max(s0, s1)
+
+
+def test_split_stages_equal_fused_solve(gpu):
+    """osc_batch_assemble + osc_batch_solve_assembled == osc_batch_solve, bit for bit."""
+    from osc_amd.solver import OSCBatchSolver
+    s = OSCBatchSolver("unitree_go2")
+    inp = generate("unitree_go2", 256, SEED_BASE + 32, "tumbling", "bernoulli")
+    args = s.prepare(**inp)
+    a = s.alloc_outputs(256, want_x=True)
+    b = s.alloc_outputs(256, want_x=True)
+    s.solve_into(a, *args)
+    s.assemble_into(b, *args)
+    s.solve_assembled_into(b, args[5])
+    torch.cuda.synchronize()
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k

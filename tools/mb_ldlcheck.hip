@@ -20,7 +20,7 @@ __global__ void k_check(const double* K, const double* r, double* x, double* F) 
   if (l + kRow < N) sdg[grp][l + kRow] = Kg[j1 * N + j1];
   __syncthreads();
   double d0, d1;
-  ldl_rows<N>(c0, c1, d0, d1, sdg[grp], l);  // d0/d1 = 1/D
+  ldl_rows<N>(c0, c1, d0, d1, 1e-13 * Kg[l * N + l], 1e-13 * Kg[j1 * N + j1]);  // d0/d1 = 1/D
   for (int i = 0; i < N; ++i) {
     F[grp * N * N + i * N + l] = c0[i];
     if (l + kRow < N) F[grp * N * N + i * N + l + kRow] = c1[i];
