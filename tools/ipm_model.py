@@ -89,8 +89,19 @@ def ldl_solve(F, r):
 
 def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
     m = len(h)
-    K0 = Hr + G.T @ G
-    y = np.linalg.solve(K0, -g + G.T @ h)
+    small = np.abs(h) < 1e3
+    if "y0_nofz" in variant:                   # least-squares start without the fz <= big rows
+        keep = ~np.isclose(h, BIG_NUMBER)
+        Gs, hs = G[keep], h[keep]
+        y = np.linalg.solve(Hr + Gs.T @ Gs, -g + Gs.T @ hs)
+    elif "y0_small" in variant:                # least-squares start over the |h| < 1e3 rows only
+        Gs, hs = G[small], h[small]
+        y = np.linalg.solve(Hr + Gs.T @ Gs, -g + Gs.T @ hs)
+    elif "y0_unc" in variant:                  # unconstrained minimiser
+        y = np.linalg.solve(Hr, -g)
+    else:
+        K0 = Hr + G.T @ G
+        y = np.linalg.solve(K0, -g + G.T @ h)
     zr = G @ y - h
     if "mehrotra_init" in variant:
         s, lam = -zr.copy(), zr.copy()
@@ -98,6 +109,25 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         s += ds_; lam += dl_
         sl = s @ lam
         s += 0.5 * sl / lam.sum(); lam += 0.5 * sl / s.sum()
+    elif "init_row1" in variant:               # per-row: slack and multiplier each >= 1
+        s, lam = np.maximum(-zr, 1.0), np.maximum(zr, 1.0)
+    elif "init_rowc" in variant:               # per-row slack; lambda centred on mu0
+        s = np.maximum(-zr, 1.0)
+        lam = np.maximum(zr, 1.0 / s)
+    elif "init_rowc10" in variant:
+        s = np.maximum(-zr, 1.0)
+        lam = np.maximum(zr, 10.0 / s)
+    elif any(v.startswith("init_rowm") for v in variant):   # shift over |h| < 1e3 rows only
+        v = [v for v in variant if v.startswith("init_rowm")][0]
+        c = float(v[9:]) if len(v) > 9 else 1.0
+        small = np.abs(h) < 1e3
+        ap = max(-(-zr[small]).min(), 0.0); ad = max(-zr[small].min(), 0.0)
+        s = np.maximum(-zr + ap + c, c)
+        lam = np.maximum(zr + ad + c, c * c / s)
+        if "mcorr" in variant:                 # Mehrotra's second shift (centering)
+            sl = s[small] @ lam[small]
+            s[small] += 0.5 * sl / lam[small].sum()
+            lam[small] += 0.5 * sl / s[small].sum()
     elif any(v.startswith("shift") for v in variant):
         c = [float(v[5:]) for v in variant if v.startswith("shift")][0]
         ap, ad = -(-zr).min(), -zr.min()
@@ -141,11 +171,21 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         dy, ds, dl = direction(s * lam)
         a_aff = max_step(ds, dl)
         mu_aff = (s + a_aff * ds) @ (lam + a_aff * dl) / m
-        sig = (mu_aff / mu) ** 3
-        rc = s * lam + ds * dl - sig * mu
+        sig = (mu_aff / mu) ** (2 if "sig2" in variant else 3)
+        so = 1.0
+        for v in variant:
+            if v.startswith("soguard"):       # drop the second-order term after a short affine step
+                if a_aff < float(v[7:]):
+                    so = 0.0
+            if v.startswith("sigfloor"):      # sigma >= c after a short affine step
+                if a_aff < 0.1:
+                    sig = max(sig, float(v[8:]))
+        if "sigcap" in variant:
+            sig = min(sig, 0.5)
+        rc = s * lam + so * ds * dl - sig * mu
         dy, ds, dl = direction(rc)
         a = max_step(ds, dl)
-        if "gondzio" in variant:
+        if "gondzio" in variant or ("gshort" in variant and a < 0.5):
             # one centrality corrector (Gondzio 1996): push complementarity products into a box
             at = min(1.0, 1.5 * a + 0.1)
             st, lt = s + at * ds, lam + at * dl
@@ -178,7 +218,8 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
 def main():
     robot = sys.argv[1] if len(sys.argv) > 1 else "unitree_go2"
     nenv = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    variants = [tuple(v.split("+")) if v != "base" else () for v in (sys.argv[3:] or ["base"])]
+    vs = [a for a in sys.argv[3:] if not a.startswith("--")]
+    variants = [tuple(v.split("+")) if v != "base" else () for v in (vs or ["base"])]
     model = load_model(robot)
     d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
     probs = [reduce_qp(model, *(d[k][e] for k in ("M", "C", "J", "b", "T", "mask")))
@@ -191,6 +232,8 @@ def main():
             its.append(it)
             errs.append(np.abs(y - yr).max() / max(np.abs(yr).max(), 1.0))
         its = np.array(its)
+        if "--hist" in sys.argv:
+            print("   hist", np.bincount(its).tolist())
         print(f"{'+'.join(v) or 'base':24s} fail {int((its >= 40).sum())} mean_it {its.mean():6.2f}  wave4_max "
               f"{its.reshape(-1, 4).max(1).mean():6.2f}  max_it {its.max():3d}  "
               f"max_err {max(errs):.2e}")
