@@ -39,6 +39,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <type_traits>
@@ -111,21 +112,34 @@ struct Dims {
   static constexpr int SMEM = O_MASK + even(NC);
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
-  // ---- IPM-kernel LDS per env (doubles): workspace prefix [g | U] + vectors.  Hr is NOT in
-  // LDS: each lane streams its two Hr columns from the (L2-resident) workspace straight into
-  // the Newton-matrix registers once per iteration, which keeps the LDS footprint small
-  // enough for two waves per SIMD. ----
-  static constexpr int I_G = W_G, I_U = W_U;
-  static constexpr int I_VY = W_HR;                    // y (current iterate)
+};
+
+// ---- IPM-kernel LDS per env (doubles): workspace prefix [g | U (| Hr)] + vectors.
+// Large batches (two waves per SIMD): Hr is NOT in LDS -- each lane streams its two Hr columns
+// from the L2-resident workspace into the Newton-matrix registers once per iteration, which
+// keeps the footprint small enough for two waves per SIMD.  Small batches (every wavefront
+// resident at once, one per SIMD): Hr joins the LDS copy when four waves' worth fits in a CU's
+// 160 KB, taking the L2 round trip off every iteration's critical path. ----
+template <class D, bool HRL>
+struct IpmLayout {
+  static constexpr int NY = D::NY, NU = D::NU, NC = D::NC, NB = D::NB;
+  static constexpr int I_G = D::W_G, I_U = D::W_U;
+  static constexpr int I_HR = D::W_HR;                 // valid when HRL
+  static constexpr int STAGE = HRL ? D::W_X : D::W_HR; // workspace prefix copied to LDS
+  static constexpr int I_VY = STAGE;                   // y (current iterate)
   static constexpr int I_VY2 = I_VY + even(NY);        // search direction
   static constexpr int I_UV = I_VY2 + even(NY);        // U_y v for the torque rows
   static constexpr int I_VR = I_UV + even(NU);         // a row-space vector
-  static constexpr int I_DR = I_VR + NRL * kRow;       // lambda / s
-  static constexpr int I_MASK = I_DR + NRL * kRow;
+  static constexpr int I_DR = I_VR + D::NRL * kRow;    // lambda / s
+  static constexpr int I_MASK = I_DR + D::NRL * kRow;
   static constexpr int I_TAU = I_MASK + even(NC);
   static constexpr int I_XB = I_TAU + even(NU);
   static constexpr int IL = I_XB + even(NB);
 };
+template <class D>
+constexpr bool hr_fits_lds() {   // four one-wave workgroups per CU, 160 KB of LDS
+  return IpmLayout<D, true>::IL * 8 * kEnvPerWave * 4 <= 160 * 1024;
+}
 
 // Upper-triangle pair tables (i <= j), built at compile time.
 template <int N, bool SKIP_CORNER>
@@ -636,21 +650,23 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   a1 = -x1;
 }
 
-template <class D>
-__global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
+template <class D, bool SMALL>
+__global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
-  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * D::IL];
+  constexpr bool HRL = SMALL && hr_fits_lds<D>();
+  using LY = IpmLayout<D, HRL>;
+  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * LY::IL];
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
   const int env_raw = blockIdx.x * kEnvPerWave + grp;
   const bool valid = env_raw < nenv;
   const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
 
-  double* B = sm + grp * D::IL;
+  double* B = sm + grp * LY::IL;
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -658,21 +674,22 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
       ws + static_cast<size_t>(blockIdx.x) * kEnvPerWave * D::WS + D::W_HR;   // L2-resident
   const unsigned lane_off = static_cast<unsigned>(env - static_cast<int>(blockIdx.x) * kEnvPerWave) *
                             static_cast<unsigned>(D::WS);
-  double* sG = B + D::I_G;
-  double* sU = B + D::I_U;
-  double* sVy = B + D::I_VY;
-  double* sVy2 = B + D::I_VY2;
-  double* sUv = B + D::I_UV;
-  double* sVr = B + D::I_VR;
-  double* sDr = B + D::I_DR;
-  double* sMask = B + D::I_MASK;
-  double* sTau = B + D::I_TAU;
-  double* sXb = B + D::I_XB;
+  double* sG = B + LY::I_G;
+  double* sU = B + LY::I_U;
+  double* sVy = B + LY::I_VY;
+  double* sVy2 = B + LY::I_VY2;
+  double* sUv = B + LY::I_UV;
+  double* sVr = B + LY::I_VR;
+  double* sDr = B + LY::I_DR;
+  double* sMask = B + LY::I_MASK;
+  double* sTau = B + LY::I_TAU;
+  double* sXb = B + LY::I_XB;
 
   STAMP_DECL
   STAMP_BEGIN();
   // stage [g | U] (the workspace prefix has the LDS layout) and the mask
-  stage(B, ws + static_cast<size_t>(env) * D::WS, D::W_HR, l, kRow);
+  stage(B, ws + static_cast<size_t>(env) * D::WS, LY::STAGE, l, kRow);
+  const double* sHr = B + LY::I_HR;
   for (int i = l; i < NC; i += kRow) sMask[i] = gmask[static_cast<size_t>(env) * NC + i];
   wave_sync();
 
@@ -782,18 +799,27 @@ __global__ __launch_bounds__(kWave, 2) void osc_ipm_kernel(
   auto load_hr = [&]() {
     // column bases formed here, every time (hidden from loop-invariant hoisting): kept live
     // across the loop they get spilled, and spill reloads wait on vmcnt(0)
-    unsigned off = lane_off;
-    asm volatile("" : "+v"(off));
-    const double* p0 = wsw + off + j0;
-    const double* p1 = wsw + off + jj1;
+    if constexpr (HRL) {
 #pragma unroll
-    for (int i = 0; i < NY; ++i) {
-      c0[i] = p0[i * NY];
-      c1[i] = p1[i * NY];
+      for (int i = 0; i < NY; ++i) {
+        c0[i] = sHr[i * NY + j0];
+        c1[i] = sHr[i * NY + jj1];
+      }
+    } else {
+      unsigned off = lane_off;
+      asm volatile("" : "+v"(off));
+      const double* p0 = wsw + off + j0;
+      const double* p1 = wsw + off + jj1;
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        c0[i] = p0[i * NY];
+        c1[i] = p1[i * NY];
+      }
     }
   };
-  const double hdg0 = wsw[lane_off + static_cast<unsigned>(j0 * NY + j0)];
-  const double hdg1 = wsw[lane_off + static_cast<unsigned>(jj1 * NY + jj1)];
+  const double hdg0 = HRL ? sHr[j0 * NY + j0] : wsw[lane_off + static_cast<unsigned>(j0 * NY + j0)];
+  const double hdg1 =
+      HRL ? sHr[jj1 * NY + jj1] : wsw[lane_off + static_cast<unsigned>(jj1 * NY + jj1)];
   load_hr();
   const double g0 = sG[j0], g1 = sG[jj1];
   double y0 = 0.0, y1 = 0.0;
@@ -1073,6 +1099,7 @@ struct osc_model {
   KernelId kid;
   DevParams* dparams;
   int device;
+  int small_batch_max;   // envs that fit one wavefront per SIMD (4 per wave x 4 SIMDs x CUs)
 };
 
 extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
@@ -1124,6 +1151,15 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   m->kid = kid;
   m->dparams = nullptr;
   (void)hipGetDevice(&m->device);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess)
+    cus = 0;
+  // One-wave-per-SIMD variant up to the batch that fills every SIMD once; beyond it the
+  // two-waves variant, except for the 32-column WaLTER system, whose Newton matrix does not fit
+  // two waves' register budget (scratch spills): it always runs one wave per SIMD with AGPR
+  // spill space (MI355X, 32,768 envs: 2.61 vs 2.95 ms; tools/variant_sweep.sh).
+  m->small_batch_max = (kid == K_WALTER) ? INT32_MAX : kEnvPerWave * 4 * cus;
+  if (const char* e = std::getenv("OSC_SMALL_BATCH_MAX")) m->small_batch_max = std::atoi(e);
   if (hipMalloc(&m->dparams, sizeof(DevParams)) != hipSuccess ||
       hipMemcpy(m->dparams, &hp, sizeof(DevParams), hipMemcpyHostToDevice) != hipSuccess) {
     if (m->dparams) (void)hipFree(m->dparams);
@@ -1173,9 +1209,15 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
                        model->dparams, nenv, M, C, J, b, T, mask, ws);
   if (stages & kInteriorPoint) {
+    // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one
+    // wave per SIMD, Hr in LDS where it fits); otherwise the two-waves-per-SIMD variant.
     const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
-    hipLaunchKernelGGL(osc_ipm_kernel<D>, dim3(nb), dim3(kWave), 0, s, model->dparams, nenv,
-                       mask, ws, tau, x, status, iters);
+    if (nenv <= model->small_batch_max)
+      hipLaunchKernelGGL((osc_ipm_kernel<D, true>), dim3(nb), dim3(kWave), 0, s, model->dparams,
+                         nenv, mask, ws, tau, x, status, iters);
+    else
+      hipLaunchKernelGGL((osc_ipm_kernel<D, false>), dim3(nb), dim3(kWave), 0, s, model->dparams,
+                         nenv, mask, ws, tau, x, status, iters);
   }
 }
 

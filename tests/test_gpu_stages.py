@@ -97,3 +97,22 @@ def test_split_stages_equal_fused_solve(gpu):
     torch.cuda.synchronize()
     for k in ("tau", "x", "status", "iters"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
+def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
+    """The one-wave-per-SIMD variant (Hr in LDS where it fits, AGPR spill space) and the
+    two-waves variant (Hr streamed from L2) run the same arithmetic: identical outputs."""
+    from osc_amd.solver import OSCBatchSolver
+    inp = generate(robot, 512, SEED_BASE + 33, "tumbling", "bernoulli")
+    outs = []
+    for force in ("100000000", "0"):
+        monkeypatch.setenv("OSC_SMALL_BATCH_MAX", force)
+        s = OSCBatchSolver(robot)
+        args = s.prepare(**inp)
+        o = s.alloc_outputs(512, want_x=True)
+        s.solve_into(o, *args)
+        torch.cuda.synchronize()
+        outs.append(o)
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(outs[0], k), getattr(outs[1], k)), k

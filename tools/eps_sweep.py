@@ -42,7 +42,8 @@ for eps in EPS:
             ref = g["x"][e]
             err = max(err, float(np.abs(x[e] - ref).max() / max(np.abs(ref).max(), 1.0)))
     row["golden_max_norm_err"] = err
-    for robot, nenv in [("unitree_go2", 4096), ("unitree_go2", 65536), ("walter_sr", 4096)]:
+    for robot, nenv in [("unitree_go2", 4096), ("unitree_go2", 65536), ("walter_sr", 4096),
+                        ("walter_sr", 32768)]:
         s = OSCBatchSolver(robot, eps_mu=eps)
         d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
         args = s.prepare(**d)
