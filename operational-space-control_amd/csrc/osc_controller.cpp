@@ -1,0 +1,245 @@
+// osc_controller.cpp -- OperationalSpaceController over the batched C-ABI (include/osc_controller.h).
+//
+// Mirrors unitree_go2/operational_space_controller.h (paths relative to the reference's
+// operational-space-control/ directory): lifecycle and preconditions :112-218, shared-state
+// accessors under one mutex :220-238, control_loop :546-589.  The QP tick itself is
+// osc_batch_solve with nenv = 1 on a private HIP stream.
+#include "osc_controller.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cstring>
+#include <iostream>
+#include <utility>
+
+namespace osc_amd {
+namespace {
+
+Status from_osc(int rc, const char* what) {
+  if (rc == OSC_OK) return Status::Ok();
+  std::string m = std::string(what) + ": " + osc_status_string(rc);
+  if (rc == OSC_ERR_INVALID_ARGUMENT || rc == OSC_ERR_UNSUPPORTED_DIMS)
+    return InvalidArgumentError(m);
+  return InternalError(m);   // IO, DEVICE, NO_DEVICE (osc.h:117 uses InternalError for loads)
+}
+
+constexpr size_t even(size_t n) { return (n + 1) & ~size_t(1); }
+
+}  // namespace
+
+OperationalSpaceController::OperationalSpaceController(std::string robot, std::string yaml_path,
+                                                       KinematicsFn kinematics,
+                                                       int control_rate_us)
+    : robot_(std::move(robot)),
+      yaml_path_(std::move(yaml_path)),
+      kinematics_(std::move(kinematics)),
+      control_rate_us_(control_rate_us) {}
+
+OperationalSpaceController::~OperationalSpaceController() {
+  if (thread_initialized_ && thread_.joinable()) {
+    running_ = false;
+    thread_.join();
+  }
+  release_device();
+}
+
+Status OperationalSpaceController::initialize(State initial_state) {
+  // The reference loads the MuJoCo XML and resolves site/body ids here (:112-160); the QP's
+  // static data comes from the YAML the reference's autogen.py reads at build time.
+  const int rc = osc_desc_from_yaml(robot_.c_str(), yaml_path_.empty() ? nullptr : yaml_path_.c_str(),
+                                    &desc_);
+  if (rc != OSC_OK) return InternalError(std::string("Failed to load OSC config: ") + osc_status_string(rc));
+  nv_ = desc_.nv;
+  nu_ = desc_.nu;
+  nc_ = desc_.nc;
+  ns_ = desc_.ns;
+  n_ = nv_ + nu_ + 3 * nc_;
+  if (initial_state.contact_mask.size() != static_cast<size_t>(nc_))
+    return InvalidArgumentError("State.contact_mask must have one entry per contact site");
+  if (!kinematics_) return InvalidArgumentError("no kinematics provider");
+  std::lock_guard<std::mutex> lock(mutex_);
+  state_ = std::move(initial_state);
+  targets_.assign(static_cast<size_t>(ns_) * 6, 0.0);   // TaskspaceTargets::Zero()  (:243)
+  torque_.assign(nu_, 0.0);                               // torque_command Zero      (:244)
+  solution_.assign(n_, 0.0);
+  initialized_ = true;
+  return Status::Ok();
+}
+
+Status OperationalSpaceController::initialize_optimization() {
+  if (!initialized_) return FailedPreconditionError("Operational Space Controller not initialized.");
+  if (optimization_initialized_) return Status::Ok();
+  Status st = from_osc(osc_model_create(&desc_, &model_), "osc_model_create");
+  if (!st.ok()) return st;
+  const size_t s = 6 * static_cast<size_t>(ns_);
+  const size_t in_doubles = even(nv_ * nv_) + even(nv_) + even(s * nv_) + even(s) +
+                            even(ns_ * 6) + even(nc_);
+  if (osc_workspace_bytes(model_, 1, &ws_bytes_) != OSC_OK) return InternalError("workspace size");
+  hipStream_t stream = nullptr;
+  if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_in_), in_doubles * sizeof(double)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_out_), (even(nu_) + even(n_)) * sizeof(double)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_info_), 2 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&d_ws_, ws_bytes_) != hipSuccess) {
+    stream_ = stream;
+    release_device();
+    return InternalError("device allocation failed");
+  }
+  stream_ = stream;
+  h_in_.assign(in_doubles, 0.0);
+  optimization_initialized_ = true;
+  return Status::Ok();
+}
+
+Status OperationalSpaceController::initialize_thread() {
+  if (!initialized_ || !optimization_initialized_)
+    return FailedPreconditionError(
+        "Initialization precoditions not met. Initialize controller and optimization before "
+        "starting control thread.");
+  running_ = true;
+  thread_ = std::thread(&OperationalSpaceController::control_loop, this);
+  thread_initialized_ = true;
+  return Status::Ok();
+}
+
+Status OperationalSpaceController::stop_thread() {
+  if (!thread_initialized_) return FailedPreconditionError("Operation Space Control Thread not initialized");
+  running_ = false;
+  if (thread_.joinable()) thread_.join();
+  return Status::Ok();
+}
+
+Status OperationalSpaceController::clean_up() {
+  if (!initialized_)
+    return FailedPreconditionError("Operational Space Controller not initialized. Nothing to clean up");
+  if (thread_initialized_ && thread_.joinable()) {
+    running_ = false;
+    thread_.join();
+  }
+  release_device();
+  optimization_initialized_ = false;
+  return Status::Ok();
+}
+
+void OperationalSpaceController::update_state(const State& new_state) {
+  std::lock_guard<std::mutex> lock(mutex_);
+  state_ = new_state;
+}
+
+void OperationalSpaceController::update_taskspace_targets(const std::vector<double>& targets) {
+  std::lock_guard<std::mutex> lock(mutex_);
+  targets_ = targets;
+}
+
+std::vector<double> OperationalSpaceController::get_torque_command() {
+  std::lock_guard<std::mutex> lock(mutex_);
+  return torque_;
+}
+
+std::vector<double> OperationalSpaceController::get_solution() {
+  std::lock_guard<std::mutex> lock(mutex_);
+  return solution_;
+}
+
+int OperationalSpaceController::last_solve_status() {
+  std::lock_guard<std::mutex> lock(mutex_);
+  return status_;
+}
+
+int OperationalSpaceController::last_iterations() {
+  std::lock_guard<std::mutex> lock(mutex_);
+  return iters_;
+}
+
+Status OperationalSpaceController::step() {
+  if (!optimization_initialized_) return FailedPreconditionError("Optimization not initialized.");
+  std::lock_guard<std::mutex> lock(mutex_);
+  return tick_locked();
+}
+
+// The body of the reference's control_loop (:556-574), caller holds the mutex.
+Status OperationalSpaceController::tick_locked() {
+  Status st = kinematics_(state_, &osc_data_);          // update_mj_data + update_osc_data
+  if (!st.ok()) return st;
+  const size_t nv = nv_, s = 6 * static_cast<size_t>(ns_);
+  if (osc_data_.mass_matrix.size() != nv * nv || osc_data_.coriolis_matrix.size() != nv ||
+      osc_data_.taskspace_jacobian.size() != s * nv || osc_data_.taskspace_bias.size() != s ||
+      targets_.size() != static_cast<size_t>(ns_) * 6 ||
+      state_.contact_mask.size() != static_cast<size_t>(nc_))
+    return InvalidArgumentError("OSCData / targets / contact_mask size mismatch");
+  // pack M | C | J | b | T | mask (row-major per block, each block padded to 16 B)
+  double* h = h_in_.data();
+  const double* blocks[6] = {osc_data_.mass_matrix.data(), osc_data_.coriolis_matrix.data(),
+                             osc_data_.taskspace_jacobian.data(), osc_data_.taskspace_bias.data(),
+                             targets_.data(), state_.contact_mask.data()};
+  const size_t sizes[6] = {nv * nv, nv, s * nv, s, static_cast<size_t>(ns_) * 6,
+                           static_cast<size_t>(nc_)};
+  double* dptr[6];
+  size_t off = 0;
+  for (int k = 0; k < 6; ++k) {
+    std::memcpy(h + off, blocks[k], sizes[k] * sizeof(double));
+    dptr[k] = d_in_ + off;
+    off += even(sizes[k]);
+  }
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (hipMemcpyAsync(d_in_, h, off * sizeof(double), hipMemcpyHostToDevice, stream) != hipSuccess)
+    return InternalError("host to device copy failed");
+  double* d_tau = d_out_;
+  double* d_x = d_out_ + even(nu_);
+  st = from_osc(osc_batch_solve(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4], dptr[5],
+                                d_tau, d_x, d_info_, d_info_ + 1, d_ws_, ws_bytes_, stream_),
+                "osc_batch_solve");
+  if (!st.ok()) return st;
+  std::vector<double> out(even(nu_) + n_);
+  int32_t info[2] = {0, 0};
+  if (hipMemcpyAsync(out.data(), d_out_, out.size() * sizeof(double), hipMemcpyDeviceToHost,
+                     stream) != hipSuccess ||
+      hipMemcpyAsync(info, d_info_, sizeof(info), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return InternalError("device to host copy failed");
+  torque_.assign(out.begin(), out.begin() + nu_);            // = solution[nv : nv+nu] (:573)
+  solution_.assign(out.begin() + even(nu_), out.begin() + even(nu_) + n_);
+  status_ = info[0];
+  iters_ = info[1];
+  return Status::Ok();
+}
+
+// control_loop (:546-589): fixed-rate ticks, overrun logged and the schedule reset.
+void OperationalSpaceController::control_loop() {
+  using Clock = std::chrono::steady_clock;
+  auto next_time = Clock::now();
+  while (running_) {
+    next_time += std::chrono::microseconds(control_rate_us_);
+    {
+      std::lock_guard<std::mutex> lock(mutex_);
+      (void)tick_locked();   // the reference ignores per-tick errors (:567)
+    }
+    const auto now = Clock::now();
+    if (now < next_time) {
+      std::this_thread::sleep_until(next_time);
+    } else {
+      const auto overrun = std::chrono::duration_cast<std::chrono::microseconds>(now - next_time);
+      std::cout << "Operational Space Control Loop Execution Time Exceeded Control Rate: "
+                << overrun.count() << "us" << std::endl;
+      next_time = now;
+    }
+  }
+}
+
+void OperationalSpaceController::release_device() {
+  if (stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+  if (d_in_) (void)hipFree(d_in_);
+  if (d_out_) (void)hipFree(d_out_);
+  if (d_info_) (void)hipFree(d_info_);
+  if (d_ws_) (void)hipFree(d_ws_);
+  if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+  if (model_) (void)osc_model_destroy(model_);
+  d_in_ = d_out_ = nullptr;
+  d_info_ = nullptr;
+  d_ws_ = nullptr;
+  stream_ = nullptr;
+  model_ = nullptr;
+}
+
+}  // namespace osc_amd

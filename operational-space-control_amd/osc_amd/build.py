@@ -1,8 +1,9 @@
-"""Build the in-tree native library: libosc_batch.so (HIP kernels for gfx950 + C-ABI + YAML loader).
+"""Build the in-tree native libraries: libosc_batch.so (HIP kernels for gfx950 + C-ABI + YAML
+loader) and libosc_controller.so (the OperationalSpaceController shim over the C-ABI).
 
     python -m osc_amd.build          (from operational-space-control_amd/)
 
-Plain hipcc, no cmake: the library is two translation units.  The .so lands in
+Plain hipcc, no cmake: three translation units.  The .so files land in
 operational-space-control_amd/lib/ so that it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
@@ -15,6 +16,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 OUT = os.path.join(PKG_DIR, "lib", "libosc_batch.so")
+OUT_CTRL = os.path.join(PKG_DIR, "lib", "libosc_controller.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 
@@ -27,6 +29,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     if not force and os.path.exists(OUT):
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):
+            build_controller()
             return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [HIPCC, "-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared",
@@ -36,7 +39,23 @@ def build(verbose: bool = False, force: bool = False) -> str:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    build_controller(force=True)
     return OUT
+
+
+def build_controller(force: bool = False) -> str:
+    """Host-only C++ (HIP runtime API); links libosc_batch.so next to it via $ORIGIN."""
+    src = os.path.join(CSRC, "osc_controller.cpp")
+    hdrs = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_controller.h")]
+    if not force and os.path.exists(OUT_CTRL):
+        t_out = os.path.getmtime(OUT_CTRL)
+        if all(os.path.getmtime(p) <= t_out for p in [src, OUT] + hdrs):
+            return OUT_CTRL
+    cmd = [HIPCC, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wno-unused-result",
+           "-I", os.path.join(REPO, "include"), src, "-L", os.path.dirname(OUT), "-losc_batch",
+           "-Wl,-rpath,$ORIGIN", "-o", OUT_CTRL]
+    subprocess.run(cmd, check=True)
+    return OUT_CTRL
 
 
 if __name__ == "__main__":

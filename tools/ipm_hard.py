@@ -24,10 +24,11 @@ for robot, n in (("unitree_go2", 256), ("walter_sr", 128)):
     m = load_model(robot)
     d = generate(robot, n, SEED_BASE + 77, "tumbling", "bernoulli")
     rand += [im.reduce_qp(m, *(d[k][e] for k in KEYS))[:4] for e in range(n)]
-base = ("etam0.1", "cap1e-5", "y0_nofz")
+base = ("etam0.1", "cap1e-5", "y0_nofz", "sig2")
 for v in sys.argv[1:] or ["-"]:
     var = base + (tuple(v.split("+")) if v != "-" else ())
     hi = np.array([im.ipm(*p, variant=var)[1] for p in hard])
     ri = np.array([im.ipm(*p, variant=var)[1] for p in rand])
+    npass = None
     print(f"{v:28s} hard: fail {int((hi >= 40).sum()):3d} mean {hi.mean():5.2f} max {hi.max():2d}"
           f" | random: fail {int((ri >= 40).sum())} mean {ri.mean():5.2f} max {ri.max():2d}", flush=True)

@@ -170,6 +170,12 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
 
         dy, ds, dl = direction(s * lam)
         a_aff = max_step(ds, dl)
+        skip = [float(v[8:]) for v in variant if v.startswith("skipcorr")]
+        if skip and a_aff >= skip[0]:           # near the end: affine (Newton) step only
+            eta = min(1.0 - 1e-5, max(0.99, 1.0 - mu, 1.0 - 0.1 * (1.0 - a_aff)))
+            alpha = min(1.0, eta * a_aff)
+            y, s, lam = y + alpha * dy, s + alpha * ds, lam + alpha * dl
+            continue
         mu_aff = (s + a_aff * ds) @ (lam + a_aff * dl) / m
         sig = (mu_aff / mu) ** (2 if "sig2" in variant else 3)
         so = 1.0
