@@ -22,7 +22,8 @@ SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL = 0, 1, 2
 EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
                     "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
                     "osc_batch_solve", "osc_batch_assemble", "osc_batch_solve_assembled",
-                    "osc_status_string", "osc_abi_version")
+                    "osc_status_string", "osc_abi_version",
+                    "osc_pd_base_targets", "osc_contact_mask_from_contacts")
 
 
 class OscModelDesc(ctypes.Structure):
@@ -82,6 +83,10 @@ def lib() -> ctypes.CDLL:
     L.osc_batch_assemble.restype = ctypes.c_int
     L.osc_batch_solve_assembled.argtypes = [vp, i32] + [vp] * 5 + [vp, ctypes.c_size_t, vp]
     L.osc_batch_solve_assembled.restype = ctypes.c_int
+    L.osc_pd_base_targets.argtypes = [i32, i32] + [vp] * 5 + [i32, vp, i32, vp, vp, vp]
+    L.osc_pd_base_targets.restype = ctypes.c_int
+    L.osc_contact_mask_from_contacts.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, vp]
+    L.osc_contact_mask_from_contacts.restype = ctypes.c_int
     _lib = L
     return L
 

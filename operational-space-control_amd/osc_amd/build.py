@@ -3,7 +3,7 @@ loader) and libosc_controller.so (the OperationalSpaceController shim over the C
 
     python -m osc_amd.build          (from operational-space-control_amd/)
 
-Plain hipcc, no cmake: three translation units.  The .so files land in
+Plain hipcc, no cmake: four translation units.  The .so files land in
 operational-space-control_amd/lib/ so that it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
@@ -20,12 +20,12 @@ OUT_CTRL = os.path.join(PKG_DIR, "lib", "libosc_controller.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["osc_batch.hip", "osc_model.cpp"]
+SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_producers.hip"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    hdrs = [os.path.join(REPO, "include", "osc_batch.h")]
+    hdrs = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h")]
     if not force and os.path.exists(OUT):
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):

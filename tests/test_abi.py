@@ -12,13 +12,15 @@ from osc_amd import _lib
 from osc_qp import load_model
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "osc_batch.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h")]
 REF_CONFIG = "/root/reference/config"
 
 
 def test_library_loads_and_exports_header_symbols():
     L = _lib.lib()
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(osc_\w+)\s*\(", open(HEADER).read(), re.M))
+    declared = set()
+    for h in HEADERS:
+        declared |= set(re.findall(r"^\s*(?:int|const char\*)\s+(osc_\w+)\s*\(", open(h).read(), re.M))
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name
@@ -72,6 +74,8 @@ def test_error_codes():
     assert L.osc_batch_solve(None, 1, *([None] * 10), None, 0, None) == 1
     assert L.osc_batch_assemble(None, 1, *([None] * 6), None, 0, None) == 1
     assert L.osc_batch_solve_assembled(None, 1, *([None] * 5), None, 0, None) == 1
+    assert L.osc_pd_base_targets(1, 5, *([None] * 5), 0, None, 0, None, None, None) == 1
+    assert L.osc_contact_mask_from_contacts(1, 4, 2, None, None, 0, None, None, None) == 1
     assert L.osc_model_destroy(None) == 1
 
 
