@@ -97,19 +97,27 @@ struct Dims {
   static constexpr int W_X = W_HR + even(NY * NY);
   static constexpr int WS = W_X + NB * NY1P;
 
-  // ---- setup-kernel LDS (doubles).  R1/R2 are reused between phases. ----
-  static constexpr int R1_A = even(S * NV) + even(S) + even(NS * 6);   // J | e | T
-  static constexpr int R1_D = even(NV * NY1) + even(NY * NY);           // T1 | Hr
+  // ---- setup-kernel LDS (doubles).  R1/R2 are reused between phases.  Every matrix that the
+  // 2x2-tiled products read by column pairs (A = [J | e | 0], X, U, T1) has an even row stride,
+  // so a column pair is one 16-byte LDS read. ----
+  static constexpr int NAP = even(NA);                   // [J | e (| 0)] row stride
+  static constexpr int NA2 = NAP / 2, NY2 = NY1P / 2;    // column pairs
+  static constexpr int NBA = NA2 * (NA2 + 1) / 2;        // Ha tiles (upper triangle)
+  static constexpr int NBT = (NV / 2) * NY2;             // T1 tiles
+  static constexpr int NBH = NY2 * (NY2 + 1) / 2;        // Hr | g tiles (upper triangle)
+  static constexpr int R1_A = S * NAP;                                  // A = [J | e | 0]
+  static constexpr int R1_D = NV * NY1P + even(NY * NY);                // T1 | Hr
   static constexpr int R1 = cmax(R1_A, R1_D);
   static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
-  static constexpr int O_J = 0, O_E = even(S * NV), O_T = O_E + even(S);
-  static constexpr int O_T1 = 0, O_HR = even(NV * NY1);
+  static constexpr int O_A = 0;
+  static constexpr int O_T1 = 0, O_HR = NV * NY1P;
   static constexpr int O_M = R1, O_C = R1 + even(NV * NV), O_G = R1;
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
   static constexpr int O_U = O_X + NB * NY1P;
   static constexpr int O_MASK = O_U + NU * NY1P;
   static constexpr int SMEM = O_MASK + even(NC);
+  static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
 };
@@ -340,9 +348,8 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   const int lane = threadIdx.x;
   if (env >= nenv) return;
 
-  double* sJ = sm + D::O_J;
-  double* sE = sm + D::O_E;
-  double* sT = sm + D::O_T;
+  constexpr int NAP = D::NAP;
+  double* sA = sm + D::O_A;
   double* sM = sm + D::O_M;
   double* sC = sm + D::O_C;
   double* sHa = sm + D::O_HA;
@@ -354,34 +361,52 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   double* sG = sm + D::O_G;
 
   // ---------------- Phase A: stage this env's inputs HBM -> LDS ----------------
-  stage(sJ, gJ + static_cast<size_t>(env) * S * NV, S * NV, lane);
+  {  // J rows -> A rows (stride NAP), 16 B per lane
+    const double2* src = reinterpret_cast<const double2*>(gJ + static_cast<size_t>(env) * S * NV);
+    double2* dst = reinterpret_cast<double2*>(sA);
+    for (int c = lane; c < S * NV / 2; c += kWave)
+      dst[(c / (NV / 2)) * (NAP / 2) + c % (NV / 2)] = src[c];
+  }
   stage(sM, gM + static_cast<size_t>(env) * NV * NV, NV * NV, lane);
   stage(sC, gC + static_cast<size_t>(env) * NV, NV, lane);
-  stage(sE, gb + static_cast<size_t>(env) * S, S, lane);
-  stage(sT, gT + static_cast<size_t>(env) * NS * 6, NS * 6, lane);
   stage(sMask, gmask + static_cast<size_t>(env) * NC, NC, lane);
-  wave_sync();
-  // e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]   (autogen.py:163-168)
+  // A column NV: e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168)
   for (int r = lane; r < S; r += kWave) {
     const int half = r / (3 * NS), rr = r % (3 * NS);
-    sE[r] -= sT[(rr / 3) * 6 + half * 3 + rr % 3];
+    sA[r * NAP + NV] = gb[static_cast<size_t>(env) * S + r] -
+                       gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+    if (NAP > NA) sA[r * NAP + NA] = 0.0;
   }
   wave_sync();
 
   // ---------------- Phase B: Ha = 2 [J e]' W [J e]  (H_dv block and f_dv column) -------------
   // H_dv = 2 J'WJ + 2 w_reg I,  f_dv = 2 J'W (b - t)   (autogen.py:131-238, 304-319)
-  for (int p = lane; p < D::NPA; p += kWave) {
-    const int i = kPairs<NA, false>.a[p], j = kPairs<NA, false>.b[p];
-    double acc = 0.0;
+  // One 2x2 tile of the upper triangle per lane (column pairs read as one 16-byte LDS load);
+  // each entry (i <= j) accumulates fma(w_r A_ri, A_rj) over r in order.
+  auto put_ha = [&](int i, int j, double v) {
+    if (i >= NA || j >= NA) return;
+    v *= 2.0;
+    if (i == j && i < NV) v += 2.0 * P->w_reg;
+    sHa[i * NA + j] = v;
+    sHa[j * NA + i] = v;
+  };
+  for (int p = lane; p < D::NBA; p += kWave) {
+    const int i0 = 2 * kPairs<D::NA2, false>.a[p], j0 = 2 * kPairs<D::NA2, false>.b[p];
+    double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
     for (int r = 0; r < S; ++r) {
-      const double ai = (i < NV) ? sJ[r * NV + i] : sE[r];
-      const double aj = (j < NV) ? sJ[r * NV + j] : sE[r];
-      acc = fma(P->w_row[r] * ai, aj, acc);
+      const double2 x = *reinterpret_cast<const double2*>(sA + r * NAP + i0);
+      const double2 y = *reinterpret_cast<const double2*>(sA + r * NAP + j0);
+      const double w = P->w_row[r];
+      const double wx0 = w * x.x, wx1 = w * x.y;
+      a00 = fma(wx0, y.x, a00);
+      a01 = fma(wx0, y.y, a01);
+      a10 = fma(wx1, y.x, a10);
+      a11 = fma(wx1, y.y, a11);
     }
-    acc *= 2.0;
-    if (i == j && i < NV) acc += 2.0 * P->w_reg;
-    sHa[i * NA + j] = acc;
-    sHa[j * NA + i] = acc;
+    put_ha(i0, j0, a00);
+    put_ha(i0, j0 + 1, a01);
+    if (i0 != j0) put_ha(i0 + 1, j0, a10);   // diagonal tile: (i0+1, i0) mirrors a01
+    put_ha(i0 + 1, j0 + 1, a11);
   }
 
   // ---------------- Phase C: base-block elimination  X = M_bb^-1 [-M_ba | Jc_b | -C_b] -------
@@ -396,7 +421,7 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     for (int i = 0; i < NB; ++i) {
       double r;
       if (c < NU) r = -sM[i * NV + NB + c];
-      else if (c < NY) r = sJ[(JC0 + c - NU) * NV + i];
+      else if (c < NY) r = sA[(JC0 + c - NU) * NAP + i];
       else r = -sC[i];
       x[i] = pinned ? 0.0 : r;
     }
@@ -434,39 +459,52 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     for (int a = 0; a < NU; ++a) {
       double acc;
       if (c < NU) acc = sM[(NB + a) * NV + NB + c];
-      else if (c < NY) acc = -sJ[(JC0 + c - NU) * NV + NB + a];
+      else if (c < NY) acc = -sA[(JC0 + c - NU) * NAP + NB + a];
       else acc = sC[NB + a];
       if (pinned) acc = 0.0;
 #pragma unroll
       for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
       sU[a * NY1P + c] = acc;
     }
+  } else if (lane < NY1P) {   // padding column of X and U: read by the 2x2 tiles, must be 0
+#pragma unroll
+    for (int i = 0; i < NB; ++i) sX[i * NY1P + lane] = 0.0;
+    for (int a = 0; a < NU; ++a) sU[a * NY1P + lane] = 0.0;
   }
   wave_sync();   // J, M, C dead from here on (R1, R2 get reused)
 
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
   // dv = Pm [y;1] with Pm = [X ; (I_nu 0 0)],  T1 = H_dv Pm (+ f_dv in the affine column),
   // Hr = Pm' T1 + 2 (w_tau + w_reg) U'U + 2 w_reg I_z,   g = last column.
-  for (int idx = lane; idx < NV * NY1; idx += kWave) {
-    const int r = idx / NY1, c = idx % NY1;
-    double acc = (c < NU) ? sHa[r * NA + NB + c] : ((c == NY) ? sHa[r * NA + NV] : 0.0);
+  // T1 = H_dv Pm: one 2x2 tile (rows r0, r0+1 x columns c0, c0+1) per lane and round.
+  auto t1_base = [&](int r, int c) -> double {
+    return (c < NU) ? sHa[r * NA + NB + c] : ((c == NY) ? sHa[r * NA + NV] : 0.0);
+  };
+  for (int p = lane; p < D::NBT; p += kWave) {
+    const int r0 = 2 * (p / D::NY2), c0 = 2 * (p % D::NY2);
+    double t00 = t1_base(r0, c0), t01 = t1_base(r0, c0 + 1);
+    double t10 = t1_base(r0 + 1, c0), t11 = t1_base(r0 + 1, c0 + 1);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) acc = fma(sHa[r * NA + i], sX[i * NY1P + c], acc);
-    sT1[r * NY1 + c] = acc;
+    for (int i = 0; i < NB; ++i) {
+      const double h0 = sHa[r0 * NA + i], h1 = sHa[(r0 + 1) * NA + i];
+      const double2 x = *reinterpret_cast<const double2*>(sX + i * NY1P + c0);
+      t00 = fma(h0, x.x, t00);
+      t01 = fma(h0, x.y, t01);
+      t10 = fma(h1, x.x, t10);
+      t11 = fma(h1, x.y, t11);
+    }
+    *reinterpret_cast<double2*>(sT1 + r0 * NY1P + c0) = make_double2(t00, t01);
+    *reinterpret_cast<double2*>(sT1 + (r0 + 1) * NY1P + c0) = make_double2(t10, t11);
   }
   wave_sync();
   {
+    // Hr | g = Pm' T1 + 2 (w_tau + w_reg) U'U (+ 2 w_reg I_z): one 2x2 tile of the upper
+    // triangle per lane and round; each entry (a <= b) accumulates X[r][a] T1[r][b] and
+    // U[q][a] U[q][b] in order.
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
-    for (int p = lane; p < D::NPH; p += kWave) {
-      const int a = kPairs<NY1, true>.a[p], b = kPairs<NY1, true>.b[p];
-      double acc = (a < NU) ? sT1[(NB + a) * NY1 + b] : 0.0;
-#pragma unroll
-      for (int r = 0; r < NB; ++r) acc = fma(sX[r * NY1P + a], sT1[r * NY1 + b], acc);
-      double uu = 0.0;
-#pragma unroll
-      for (int q = 0; q < NU; ++q) uu = fma(sU[q * NY1P + a], sU[q * NY1P + b], uu);
-      acc = fma(wu2, uu, acc);
+    auto put_hr = [&](int a, int b, double acc) {
+      if (b >= NY1 || (a == NY && b == NY)) return;
       if (b < NY) {
         if (a == b && a >= NU) {
           acc += wr2;
@@ -477,6 +515,39 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
       } else {
         sG[a] = acc;
       }
+    };
+    for (int p = lane; p < D::NBH; p += kWave) {
+      const int a0 = 2 * kPairs<D::NY2, false>.a[p], b0 = 2 * kPairs<D::NY2, false>.b[p];
+      double h[2][2], uu[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          h[i][j] = (a0 + i < NU) ? sT1[(NB + a0 + i) * NY1P + b0 + j] : 0.0;
+          uu[i][j] = 0.0;
+        }
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const double2 xa = *reinterpret_cast<const double2*>(sX + r * NY1P + a0);
+        const double2 tb = *reinterpret_cast<const double2*>(sT1 + r * NY1P + b0);
+        h[0][0] = fma(xa.x, tb.x, h[0][0]);
+        h[0][1] = fma(xa.x, tb.y, h[0][1]);
+        h[1][0] = fma(xa.y, tb.x, h[1][0]);
+        h[1][1] = fma(xa.y, tb.y, h[1][1]);
+      }
+#pragma unroll
+      for (int q = 0; q < NU; ++q) {
+        const double2 ua = *reinterpret_cast<const double2*>(sU + q * NY1P + a0);
+        const double2 ub = *reinterpret_cast<const double2*>(sU + q * NY1P + b0);
+        uu[0][0] = fma(ua.x, ub.x, uu[0][0]);
+        uu[0][1] = fma(ua.x, ub.y, uu[0][1]);
+        uu[1][0] = fma(ua.y, ub.x, uu[1][0]);
+        uu[1][1] = fma(ua.y, ub.y, uu[1][1]);
+      }
+      put_hr(a0, b0, fma(wu2, uu[0][0], h[0][0]));
+      put_hr(a0, b0 + 1, fma(wu2, uu[0][1], h[0][1]));
+      if (a0 != b0) put_hr(a0 + 1, b0, fma(wu2, uu[1][0], h[1][0]));
+      put_hr(a0 + 1, b0 + 1, fma(wu2, uu[1][1], h[1][1]));
     }
   }
   wave_sync();
