@@ -913,23 +913,34 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   //   (Hr + G'G) y0 = -g + G'h,  s = h - G y0,  lambda = G y0 - h,  both shifted positive.
   // The four environments of the wave iterate in lockstep; a converged one stops moving
   // (step 0) until the slowest has converged.
+  // Primal residual rp = G y + s - h.  Every step takes ds = -rp - G dy exactly, so the new
+  // residual is (1 - alpha) rp up to rounding, whatever the accuracy of the linear solve: it is
+  // carried while mu > 1e-6 and formed from scratch after the initial point and once mu is
+  // small, where the ~1e-12 rounding the carried value ignores is as large as the active
+  // slacks (tools/ipm_model.py "rpcarry1e-6": same iterations as recomputing every time).
+  // rd, which does depend on the solve's accuracy, is recomputed every iteration.
+  double rp[NRL];
+#pragma unroll
+  for (int t = 0; t < NRL; ++t) rp[t] = 0.0;
   for (int it = -1;; ++it) {
     STAMP_BEGIN();
     const bool init = it < 0;
-    double rp[NRL];
     double mu = 0.0;
-#pragma unroll
-    for (int t = 0; t < NRL; ++t) rp[t] = 0.0;
     if (!init) {
-      uv_product(sVy);
-      wave_sync();
       double cs = 0.0;
 #pragma unroll
-      for (int t = 0; t < NRL; ++t) {
-        rp[t] = act[t] ? Gv(sVy, t) + s[t] - h[t] : 0.0;
-        cs += act[t] ? s[t] * lam[t] : 0.0;
-      }
+      for (int t = 0; t < NRL; ++t) cs += act[t] ? s[t] * lam[t] : 0.0;
       mu = row_sum(cs) / fmax(m_act, 1.0);
+      const bool fresh = it == 0 || mu <= 1e-6;
+      if (__ballot(fresh) != 0) {   // wave-uniform: the product uses the whole row's lanes
+        uv_product(sVy);
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          const double r = act[t] ? Gv(sVy, t) + s[t] - h[t] : 0.0;
+          rp[t] = fresh ? r : rp[t];
+        }
+      }
       if (!done && mu <= P->eps_mu) {
         done = true;
         st = OSC_SOLVE_OK;
@@ -1093,6 +1104,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       for (int t = 0; t < NRL; ++t) {
         s[t] = act[t] ? fma(alpha, ds[t], s[t]) : 1.0;
         lam[t] = act[t] ? fma(alpha, dl[t], lam[t]) : 0.0;
+        rp[t] *= 1.0 - alpha;
       }
     }
     sVy[j0] = y0;

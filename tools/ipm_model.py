@@ -139,8 +139,15 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         s = -zr + (1.0 + ap if ap >= 0 else 0.0)
         lam = zr + (1.0 + ad if ad >= 0 else 0.0)
     eta = 0.99
+    rp_c = None
     for it in range(max_iter + 1):
         rp = G @ y + s - h
+        thr = [float(v[7:]) for v in variant if v.startswith("rpcarry") and len(v) > 7]
+        mu_now = s @ lam / m
+        if "rpcarry" in variant or thr:
+            if rp_c is None or (thr and mu_now <= thr[0]):
+                rp_c = rp
+            rp = rp_c
         rd = Hr @ y + g + G.T @ lam
         mu = s @ lam / m
         if mu <= eps_mu:
@@ -218,6 +225,8 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
                 eta = min(eta, 1.0 - float(v[3:]))
         alpha = min(1.0, eta * a)
         y, s, lam = y + alpha * dy, s + alpha * ds, lam + alpha * dl
+        if rp_c is not None:
+            rp_c = (1.0 - alpha) * rp_c
     return y, max_iter, False
 
 
