@@ -27,8 +27,9 @@ sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from osc_amd.dist import barrier as dist_barrier, job_value, rank_info, reduce_stats, shard_seed  # noqa: E402,E501
 from osc_amd.robots import bytes_per_solve, dims  # noqa: E402
-from osc_amd.synth import SEED_BASE, generate  # noqa: E402
+from osc_amd.synth import generate  # noqa: E402
 
 METRIC = "OSC control steps/sec (batched envs), Go2 18-DoF, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -89,23 +90,21 @@ def main() -> None:
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ri = rank_info()
+    world, rank, local = ri.world, ri.rank, ri.local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev)   # RCCL; barriers + timing reduction only
 
     def barrier():
-        if world > 1:
-            torch.distributed.barrier()
+        dist_barrier(world)
 
     from osc_amd.solver import OSCBatchSolver
     nenv = args.nenv_per_gpu
     solver = OSCBatchSolver(args.robot)
-    d = generate(args.robot, nenv, SEED_BASE + 2 + 1000 * rank, args.scenario, args.mask)
+    d = generate(args.robot, nenv, shard_seed(rank), args.scenario, args.mask)
     inputs = solver.prepare(**d)
     out = solver.alloc_outputs(nenv)
     stream = torch.cuda.current_stream(dev)
@@ -137,19 +136,13 @@ def main() -> None:
 
     st = out.status.cpu().numpy()
     mean_iters = float(out.iters.double().mean().item())
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, setup_ms, ipm_ms], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kernel_ms, setup_ms, ipm_ms = (float(v) for v in t)
-        c = torch.tensor([float((st == 0).sum()), float(st.size)], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(c)
-        converged = float(c[0] / c[1])
-    else:
-        converged = float((st == 0).mean())
+    stats = reduce_stats(world, dev, nenv, elapsed, setup_ms, ipm_ms, int((st == 0).sum()))
+    elapsed, kernel_ms, setup_ms, ipm_ms = stats.elapsed_s, stats.kernel_ms, stats.setup_ms, stats.ipm_ms
+    converged = stats.converged
 
     if rank == 0:
-        total = nenv * world
-        value = total * args.steps / elapsed
+        total = stats.total_envs
+        value = job_value(stats, args.steps)
         bps = bytes_per_solve(args.robot)
         achieved = bps * nenv / (kernel_ms * 1e-3) / 1e9
         traffic = None

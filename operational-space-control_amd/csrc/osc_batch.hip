@@ -271,7 +271,7 @@ __device__ __forceinline__ double row_max(double v) {
 // ---- diagnostic stamps (OSC_STAMPS builds only; the product build compiles them out) ----
 // Per wave, cycles (s_memtime) accumulated per IPM phase; read back by osc_debug_stamps.
 #ifdef OSC_STAMPS
-constexpr int kStampSlots = 8;
+constexpr int kStampSlots = 12;
 constexpr int kStampBlocks = 1 << 15;
 __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 #define STAMP_DECL unsigned long long st_acc[kStampSlots] = {}; unsigned long long st_t0 = 0;
@@ -967,15 +967,20 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     double rd0 = g0 + GTw(sVr, j0, jk0, jc0), rd1 = g1 + GTw(sVr, jj1, jk1, jc1);
     double dg0 = hdg0, dg1 = hdg1;
     if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
+    STAMP_END(8);
+    STAMP_BEGIN();
     // U' diag(d) U: per torque row q, rank-1 update with u = U[q][.] broadcast from the lane
     // holding it (DPP) -- no broadcast LDS reads in the loop.
     // rolled (I-cache, registers); the next row's three LDS reads are issued one trip ahead
-    double du_n = sDr[0] + sDr[1], u0_n = sU[j0], u1_n = sU[jj1];
+    // (the sum of the two row weights is formed at use, not at load: adding at load time would
+    // wait for the prefetch at the top of every trip)
+    double2 dd_n = *reinterpret_cast<const double2*>(sDr);
+    double u0_n = sU[j0], u1_n = sU[jj1];
 #pragma unroll 1
     for (int q = 0; q < NU; ++q) {
-      const double du = du_n, u0 = u0_n, u1 = u1_n;
+      const double du = dd_n.x + dd_n.y, u0 = u0_n, u1 = u1_n;
       const int qn = (q + 1 < NU) ? q + 1 : q;
-      du_n = sDr[2 * qn] + sDr[2 * qn + 1];
+      dd_n = *reinterpret_cast<const double2*>(sDr + 2 * qn);
       u0_n = sU[qn * NY1P + j0];
       u1_n = sU[qn * NY1P + jj1];
       const double t0 = du * u0, t1 = du * u1;
@@ -983,6 +988,8 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       dg1 = fma(t1, u1, dg1);
       rank1_rows<NY>(c0, c1, u0, u1, t0, t1);
     }
+    STAMP_END(9);
+    STAMP_BEGIN();
     if (jk0 >= 0) {
       double a, b, cc;
       contact_col(jk0, jc0, a, b, cc);

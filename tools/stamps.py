@@ -15,8 +15,9 @@ from osc_amd import _lib  # noqa: E402
 from osc_amd.solver import OSCBatchSolver  # noqa: E402
 from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
-NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble K", "LDL^T", "rhs (2 passes)",
-         "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update"]
+NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble: contact blocks", "LDL^T",
+         "rhs (2 passes)", "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update",
+         "assemble: rd = g + G'lam + Hr y", "assemble: rank-1 U terms", "-", "-"]
 for robot in ["unitree_go2", "walter_sr"]:
     nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     s = OSCBatchSolver(robot)
@@ -26,11 +27,11 @@ for robot in ["unitree_go2", "walter_sr"]:
     s.solve_into(out, *args)
     torch.cuda.synchronize()
     nblk = nenv // 4
-    buf = (ctypes.c_ulonglong * (nblk * 8))()
+    buf = (ctypes.c_ulonglong * (nblk * len(NAMES)))()
     L = _lib.lib()
     L.osc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.osc_debug_stamps(ctypes.cast(buf, ctypes.c_void_p), nblk) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, 8).astype(np.float64)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, len(NAMES)).astype(np.float64)
     it = out.iters.cpu().numpy().reshape(nblk, 4).max(axis=1) + 1   # + init pass
     tot = a.sum(axis=1)
     per = {n: float(a[:, k].mean()) for k, n in enumerate(NAMES)}
