@@ -154,6 +154,38 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
             return y, it, True
         if it >= max_iter:
             return y, it, False
+        pol = [float(v[6:]) for v in variant if v.startswith("polish")]
+        if pol and mu <= pol[0]:
+            # active-set polish: rows with s < lambda treated as equalities, exact KKT solve
+            A = s < lam
+            GA = G[A]
+            nA = int(A.sum())
+            try:
+                if "penalty" in variant:   # kernel form: (Hr + rho GA'GA), refined 2x
+                    rho = 1e8
+                    Kp = Hr + rho * GA.T @ GA
+                    Fp = ldl_factor(Kp)
+                    yp = ldl_solve(Fp, -g + rho * GA.T @ h[A])
+                    lp = rho * (GA @ yp - h[A])
+                    for _ in range(2):
+                        r1 = -g - Hr @ yp - GA.T @ lp       # stationarity residual
+                        r2 = h[A] - GA @ yp                  # active-row residual
+                        # regularised KKT [Hr GA'; GA -1/rho] correction via the Schur form
+                        dy = ldl_solve(Fp, r1 + rho * GA.T @ r2)
+                        dl_ = rho * (GA @ dy - r2)
+                        yp, lp = yp + dy, lp + dl_
+                else:
+                    KKT = np.block([[Hr, GA.T], [GA, np.zeros((nA, nA))]])
+                    sol = np.linalg.solve(KKT, np.concatenate([-g, h[A]]))
+                    yp, lp = sol[:len(g)], sol[len(g):]
+                ptol = [float(v[4:]) for v in variant if v.startswith("ptol")]
+                ptol = ptol[0] if ptol else 1e-9
+                feas = np.all(G @ yp <= h + ptol * (1 + np.abs(h)))
+                dual = nA == 0 or np.all(lp >= -ptol * (1 + np.abs(lp).max()))
+                if feas and dual:
+                    return yp, it + 1, True
+            except np.linalg.LinAlgError:
+                pass
         D = lam / s
         K = Hr + G.T @ (D[:, None] * G)
         Kf = ldl_factor(K)
