@@ -837,17 +837,62 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   const int jk0 = (j0 >= NU) ? (j0 - NU) / 3 : -1, jc0 = (j0 >= NU) ? (j0 - NU) % 3 : 0;
   const int jk1 = (v1 && j1 >= NU) ? (j1 - NU) / 3 : -1, jc1 = (j1 >= NU) ? (j1 - NU) % 3 : 0;
   // (G' w)_j for row-space w staged in LDS (inactive rows hold 0)
-  auto GTw = [&](const double* w, int jj, int jk, int jc) -> double {
-    double acc = 0.0;
+  // (G' w)_j for both variable slots of this lane, w row-space in LDS (inactive rows hold 0).
+  // All reads are issued before the arithmetic (one wait, not one per torque row); the contact
+  // part is branch-free: each lane reads its contact's six rows (16-byte pairs) and keeps the
+  // combination of its component jc.
+  auto contact_term = [&](const double* w, int jk, int jc) -> double {
+    const double* wk = w + 2 * NU + 6 * (jk >= 0 ? jk : 0);
+    const double2 a = *reinterpret_cast<const double2*>(wk);
+    const double2 b = *reinterpret_cast<const double2*>(wk + 2);
+    const double2 c = *reinterpret_cast<const double2*>(wk + 4);
+    const double v0 = a.x - a.y + b.x - b.y;
+    const double v1 = a.x + a.y - b.x - b.y;
+    const double v2 = -mu_f * (a.x + a.y + b.x + b.y) - c.x + c.y;
+    const double v = (jc == 0) ? v0 : ((jc == 1) ? v1 : v2);
+    return jk >= 0 ? v : 0.0;
+  };
+  auto GTw2 = [&](const double* w, double& r0, double& r1) {
+    double a0 = 0.0, a1 = 0.0;
+    if constexpr (SMALL) {
+      // one wave per SIMD: latency is exposed, registers are not short (AGPR spill space)
+      double d[NU], u0[NU], u1[NU];
 #pragma unroll
-    for (int q = 0; q < NU; ++q) acc = fma(sU[q * NY1P + jj], w[2 * q] - w[2 * q + 1], acc);
-    if (jk >= 0) {
-      const double* wk = w + 2 * NU + 6 * jk;
-      if (jc == 0) acc += wk[0] - wk[1] + wk[2] - wk[3];
-      else if (jc == 1) acc += wk[0] + wk[1] - wk[2] - wk[3];
-      else acc += -mu_f * (wk[0] + wk[1] + wk[2] + wk[3]) - wk[4] + wk[5];
+      for (int q = 0; q < NU; ++q) {
+        const double2 p = *reinterpret_cast<const double2*>(w + 2 * q);   // rows 2q, 2q+1
+        d[q] = p.x - p.y;
+      }
+#pragma unroll
+      for (int q = 0; q < NU; ++q) {
+        u0[q] = sU[q * NY1P + j0];
+        u1[q] = sU[q * NY1P + jj1];
+      }
+      const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
+#pragma unroll
+      for (int q = 0; q < NU; ++q) {
+        a0 = fma(u0[q], d[q], a0);
+        a1 = fma(u1[q], d[q], a1);
+      }
+      r0 = a0 + k0;
+      r1 = a1 + k1;
+    } else {
+      // two waves per SIMD: the other wave hides the latency, registers are the limit
+      // (one slot at a time, branchy contact part: the register-lightest form)
+      auto gtw = [&](int jj, int jk, int jc) -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < NU; ++q) acc = fma(sU[q * NY1P + jj], w[2 * q] - w[2 * q + 1], acc);
+        if (jk >= 0) {
+          const double* wk = w + 2 * NU + 6 * jk;
+          if (jc == 0) acc += wk[0] - wk[1] + wk[2] - wk[3];
+          else if (jc == 1) acc += wk[0] + wk[1] - wk[2] - wk[3];
+          else acc += -mu_f * (wk[0] + wk[1] + wk[2] + wk[3]) - wk[4] + wk[5];
+        }
+        return acc;
+      };
+      r0 = gtw(j0, jk0, jc0);
+      r1 = gtw(jj1, jk1, jc1);
     }
-    return acc;
   };
   // contact block column (B[0..2][jc]) of var slot in contact jk, from D = lambda/s
   auto contact_col = [&](int jk, int jc, double& v0, double& v1_, double& v2) {
@@ -964,7 +1009,10 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     STAMP_END(1);
     STAMP_BEGIN();
     // ---- Newton matrix K = Hr + G' D G (columns j0, j1 in registers) and rd = Hr y + g + G'lam
-    double rd0 = g0 + GTw(sVr, j0, jk0, jc0), rd1 = g1 + GTw(sVr, jj1, jk1, jc1);
+    double rd0, rd1;
+    GTw2(sVr, rd0, rd1);
+    rd0 += g0;
+    rd1 += g1;
     double dg0 = hdg0, dg1 = hdg1;
     if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
     STAMP_END(8);
@@ -1032,8 +1080,9 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
         sVr[l + kRow * t] = init ? (init_ls(t) ? h[t] : 0.0) : (rc - lam[t] * rp[t]) * inv_s[t];
       }
       wave_sync();
-      dy0 = -rd0 + GTw(sVr, j0, jk0, jc0);
-      dy1 = -rd1 + GTw(sVr, jj1, jk1, jc1);
+      GTw2(sVr, dy0, dy1);
+      dy0 -= rd0;
+      dy1 -= rd1;
       STAMP_END(4);
       STAMP_BEGIN();
       ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, dy0, dy1, l);
