@@ -833,6 +833,31 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       sUv[l] = a;
     }
   };
+  // (G v)_r for all row slots at once, branch-free, every read issued first (one-wave variant):
+  // torque rows read U_y v, contact rows read their contact's three force entries.
+  auto Gv_all = [&](const double* v, double (&out)[NRL]) {
+    double uq[NRL], f0[NRL], f1[NRL], f2[NRL];
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) {
+      const int r = l + kRow * t;
+      const int q = (r < 2 * NU) ? (r >> 1) : 0;
+      const int k = (r >= 2 * NU && r < MI) ? (r - 2 * NU) / 6 : 0;
+      uq[t] = sUv[q];
+      f0[t] = v[NU + 3 * k];
+      f1[t] = v[NU + 3 * k + 1];
+      f2[t] = v[NU + 3 * k + 2];
+    }
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) {
+      const int r = l + kRow * t;
+      const int rt = (r - 2 * NU) % 6;
+      const double sx = (rt & 1) ? -1.0 : 1.0, sy = (rt >= 2) ? -1.0 : 1.0;
+      const double pyr = sx * f0[t] + sy * f1[t] - mu_f * f2[t];
+      const double crow = (rt < 4) ? pyr : ((rt == 4) ? -f2[t] : f2[t]);
+      const double trow = (r & 1) ? -uq[t] : uq[t];
+      out[t] = !act[t] ? 0.0 : ((r < 2 * NU) ? trow : crow);
+    }
+  };
   // (G v)_r for row slot t, given sUv = U_y v
   auto Gv = [&](const double* v, int t) -> double {
     if (!act[t]) return 0.0;
@@ -1111,10 +1136,12 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       wave_sync();
       // step to the boundary, division-free: 1 / max(1, max_r(-ds/s), max_r(-dl/lambda))
       double rmax = 1.0;
+      double gdy_all[NRL];
+      if constexpr (SMALL) Gv_all(sVy2, gdy_all);
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
         const double rc = fma(s[t], lam[t], dsdl[t]) - sig_mu;
-        const double gdy = Gv(sVy2, t);
+        const double gdy = SMALL ? gdy_all[t] : Gv(sVy2, t);
         ds[t] = act[t] ? -rp[t] - gdy : 0.0;
         dl[t] = -(rc + lam[t] * ds[t]) * inv_s[t];
         const double inv_l = (act[t] && !init) ? recip1(lam[t]) : 0.0;
