@@ -328,12 +328,36 @@ __device__ __forceinline__ double recip(double d) {
 }
 
 // Copy n doubles (n even, both pointers 16-byte aligned) global -> LDS, 16 B per lane.
-__device__ __forceinline__ void stage(double* dst, const double* __restrict__ src, int n, int lane,
-                                      int stride = kWave) {
-  const double2* s2 = reinterpret_cast<const double2*>(src);
-  double2* d2 = reinterpret_cast<double2*>(dst);
-  for (int i = lane; i < n / 2; i += stride) d2[i] = s2[i];
-}
+// N2 16-byte elements copied global -> LDS by STRIDE lanes, in two halves so that every load is
+// in flight before the first store (a rolled copy loop waits one memory latency per trip: the
+// IPM kernel's 28-trip staging of [g | U | Hr] used to cost ~28 L2/HBM round trips).
+template <int N2, int STRIDE>
+struct Batch2 {
+  static constexpr int T = (N2 + STRIDE - 1) / STRIDE;
+  static constexpr bool kFull = N2 % STRIDE == 0;
+  double2 v[T];
+  __device__ __forceinline__ void load(const double* __restrict__ src, int lane) {
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int i = lane + t * STRIDE;
+      v[t] = s2[(kFull || t < T - 1 || i < N2) ? i : N2 - 1];   // clamped: no branch per load
+    }
+  }
+  // dst index of element i given by map(i) (identity for a plain copy)
+  template <class Map>
+  __device__ __forceinline__ void store(double* dst, int lane, Map map) const {
+    double2* d2 = reinterpret_cast<double2*>(dst);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int i = lane + t * STRIDE;
+      if (kFull || t < T - 1 || i < N2) d2[map(i)] = v[t];
+    }
+  }
+  __device__ __forceinline__ void store(double* dst, int lane) const {
+    store(dst, lane, [](int i) { return i; });
+  }
+};
 
 // ============================ kernel 1: reduced QP per env ==================================
 template <class D>
@@ -361,21 +385,37 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   double* sG = sm + D::O_G;
 
   // ---------------- Phase A: stage this env's inputs HBM -> LDS ----------------
-  {  // J rows -> A rows (stride NAP), 16 B per lane
-    const double2* src = reinterpret_cast<const double2*>(gJ + static_cast<size_t>(env) * S * NV);
-    double2* dst = reinterpret_cast<double2*>(sA);
-    for (int c = lane; c < S * NV / 2; c += kWave)
-      dst[(c / (NV / 2)) * (NAP / 2) + c % (NV / 2)] = src[c];
-  }
-  stage(sM, gM + static_cast<size_t>(env) * NV * NV, NV * NV, lane);
-  stage(sC, gC + static_cast<size_t>(env) * NV, NV, lane);
-  stage(sMask, gmask + static_cast<size_t>(env) * NC, NC, lane);
+  // every load first (one memory latency), then the LDS stores
+  static_assert(NV % 2 == 0 && NC % 2 == 0, "16-byte staging needs even nv and nc");
+  Batch2<S * NV / 2, kWave> bJ;
+  Batch2<NV * NV / 2, kWave> bM;
+  Batch2<NV / 2, kWave> bC;
+  Batch2<NC / 2, kWave> bK;
+  bJ.load(gJ + static_cast<size_t>(env) * S * NV, lane);
+  bM.load(gM + static_cast<size_t>(env) * NV * NV, lane);
+  bC.load(gC + static_cast<size_t>(env) * NV, lane);
+  bK.load(gmask + static_cast<size_t>(env) * NC, lane);
   // A column NV: e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168)
-  for (int r = lane; r < S; r += kWave) {
+  constexpr int TE = (S + kWave - 1) / kWave;
+  double eb[TE], et[TE];
+#pragma unroll
+  for (int q = 0; q < TE; ++q) {
+    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
     const int half = r / (3 * NS), rr = r % (3 * NS);
-    sA[r * NAP + NV] = gb[static_cast<size_t>(env) * S + r] -
-                       gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
-    if (NAP > NA) sA[r * NAP + NA] = 0.0;
+    eb[q] = gb[static_cast<size_t>(env) * S + r];
+    et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+  }
+  bJ.store(sA, lane, [](int c) { return (c / (NV / 2)) * (NAP / 2) + c % (NV / 2); });   // J rows -> A rows
+  bM.store(sM, lane);
+  bC.store(sC, lane);
+  bK.store(sMask, lane);
+#pragma unroll
+  for (int q = 0; q < TE; ++q) {
+    const int r = lane + q * kWave;
+    if (r < S) {
+      sA[r * NAP + NV] = eb[q] - et[q];
+      if (NAP > NA) sA[r * NAP + NA] = 0.0;
+    }
   }
   wave_sync();
 
@@ -758,10 +798,17 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 
   STAMP_DECL
   STAMP_BEGIN();
-  // stage [g | U] (the workspace prefix has the LDS layout) and the mask
-  stage(B, ws + static_cast<size_t>(env) * D::WS, LY::STAGE, l, kRow);
+  // stage [g | U (| Hr)] (the workspace prefix has the LDS layout) and the mask: all loads in
+  // flight before the first LDS store
+  static_assert(LY::STAGE % 2 == 0 && NC <= kRow, "staging layout");
+  {
+    Batch2<LY::STAGE / 2, kRow> bs;
+    bs.load(ws + static_cast<size_t>(env) * D::WS, l);
+    const double mk = gmask[static_cast<size_t>(env) * NC + (l < NC ? l : 0)];
+    bs.store(B, l);
+    if (l < NC) sMask[l] = mk;
+  }
   const double* sHr = B + LY::I_HR;
-  for (int i = l; i < NC; i += kRow) sMask[i] = gmask[static_cast<size_t>(env) * NC + i];
   wave_sync();
 
   // ---- inequality rows of this lane: r = l + 16 t.  Only (active, h) are kept; the row's
