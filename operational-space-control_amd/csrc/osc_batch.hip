@@ -274,6 +274,7 @@ __device__ __forceinline__ double row_max(double v) {
 constexpr int kStampSlots = 12;
 constexpr int kStampBlocks = 1 << 15;
 __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
+__device__ unsigned long long g_setup_stamps[kStampBlocks * kStampSlots];
 #define STAMP_DECL unsigned long long st_acc[kStampSlots] = {}; unsigned long long st_t0 = 0;
 #define STAMP_BEGIN()                                                        \
   do {                                                                       \
@@ -295,11 +296,18 @@ __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
       for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
         g_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];                \
   } while (0)
+#define STAMP_STORE_SETUP()                                                  \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                       \
+      for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
+        g_setup_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];          \
+  } while (0)
 #else
 #define STAMP_DECL
 #define STAMP_BEGIN() do {} while (0)
 #define STAMP_END(slot) do {} while (0)
 #define STAMP_STORE() do {} while (0)
+#define STAMP_STORE_SETUP() do {} while (0)
 #endif
 
 // Both kernels run ONE wavefront per workgroup.  LDS instructions of a wavefront execute in
@@ -344,20 +352,37 @@ struct Batch2 {
       v[t] = s2[(kFull || t < T - 1 || i < N2) ? i : N2 - 1];   // clamped: no branch per load
     }
   }
-  // dst index of element i given by map(i) (identity for a plain copy)
+  // dst index of element i given by map(i) (identity for a plain copy).  Lanes past the end
+  // rewrite element N2-1 with the value they loaded for it (clamped above): no branch, so the
+  // compiler cannot sink the last trip's load into a conditional block behind earlier waits.
   template <class Map>
   __device__ __forceinline__ void store(double* dst, int lane, Map map) const {
     double2* d2 = reinterpret_cast<double2*>(dst);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const int i = lane + t * STRIDE;
-      if (kFull || t < T - 1 || i < N2) d2[map(i)] = v[t];
+      d2[map((kFull || t < T - 1 || i < N2) ? i : N2 - 1)] = v[t];
     }
   }
   __device__ __forceinline__ void store(double* dst, int lane) const {
     store(dst, lane, [](int i) { return i; });
   }
 };
+
+// p-th pair (i <= j) of the row-major upper triangle of an N x N grid -- the order of
+// Pairs<N, false> -- in closed form (no table load: a per-lane indexed constant-table read is a
+// memory round trip at the top of a phase).  i from the quadratic, then one integer correction
+// each way for the rounding of the f32 square root.
+template <int N>
+__device__ __forceinline__ void upper_pair(int p, int& i, int& j) {
+  constexpr int B = 2 * N + 1;
+  auto start = [](int r) { return r * (2 * N - r + 1) / 2; };
+  int r = static_cast<int>((B - __builtin_sqrtf(static_cast<float>(B * B - 8 * p))) * 0.5f);
+  r = (r + 1 < N && start(r + 1) <= p) ? r + 1 : r;
+  r = (r > 0 && start(r) > p) ? r - 1 : r;
+  i = r;
+  j = p - start(r) + r;
+}
 
 // ============================ kernel 1: reduced QP per env ==================================
 template <class D>
@@ -384,6 +409,8 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   double* sHr = sm + D::O_HR;
   double* sG = sm + D::O_G;
 
+  STAMP_DECL
+  STAMP_BEGIN();
   // ---------------- Phase A: stage this env's inputs HBM -> LDS ----------------
   // every load first (one memory latency), then the LDS stores
   static_assert(NV % 2 == 0 && NC % 2 == 0, "16-byte staging needs even nv and nc");
@@ -410,15 +437,15 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   bC.store(sC, lane);
   bK.store(sMask, lane);
 #pragma unroll
-  for (int q = 0; q < TE; ++q) {
-    const int r = lane + q * kWave;
-    if (r < S) {
-      sA[r * NAP + NV] = eb[q] - et[q];
-      if (NAP > NA) sA[r * NAP + NA] = 0.0;
-    }
+  for (int q = 0; q < TE; ++q) {   // lanes past S rewrite row S-1 with its own value (no branch)
+    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+    sA[r * NAP + NV] = eb[q] - et[q];
+    if (NAP > NA) sA[r * NAP + NA] = 0.0;
   }
   wave_sync();
 
+  STAMP_END(0);
+  STAMP_BEGIN();
   // ---------------- Phase B: Ha = 2 [J e]' W [J e]  (H_dv block and f_dv column) -------------
   // H_dv = 2 J'WJ + 2 w_reg I,  f_dv = 2 J'W (b - t)   (autogen.py:131-238, 304-319)
   // One 2x2 tile of the upper triangle per lane (column pairs read as one 16-byte LDS load);
@@ -431,7 +458,10 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     sHa[j * NA + i] = v;
   };
   for (int p = lane; p < D::NBA; p += kWave) {
-    const int i0 = 2 * kPairs<D::NA2, false>.a[p], j0 = 2 * kPairs<D::NA2, false>.b[p];
+    int i0, j0;
+    upper_pair<D::NA2>(p, i0, j0);
+    i0 *= 2;
+    j0 *= 2;
     double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
     for (int r = 0; r < S; ++r) {
       const double2 x = *reinterpret_cast<const double2*>(sA + r * NAP + i0);
@@ -449,22 +479,34 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     put_ha(i0 + 1, j0 + 1, a11);
   }
 
+  STAMP_END(1);
+  STAMP_BEGIN();
   // ---------------- Phase C: base-block elimination  X = M_bb^-1 [-M_ba | Jc_b | -C_b] -------
   // and the torque map U = M_a Pm + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
   // (dynamics rows: autogen.py:58-89; Jc = Jp[last 3nc rows]^T: osc.h:439-445)
   constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
-  if (lane < NY1) {
-    const int c = lane;
+  // One lane per column c of [y; 1]; when two copies of the 32-lane column set fit the wave,
+  // both halves solve for X (redundantly) and split the NU rows of U between them.
+  constexpr bool kSplitU = 2 * NY1P <= kWave;
+  constexpr int kUStep = kSplitU ? (NU + 1) / 2 : NU;
+  const int c = kSplitU ? (lane & 31) : lane;
+  const int a_lo = kSplitU ? (lane >> 5) * kUStep : 0;
+  if (c < NY1) {
     const bool pinned = (c >= NU && c < NY) && (sMask[(c - NU) / 3] == 0.0);
+    // right-hand side and U's constant term are strided LDS vectors chosen per lane (no
+    // divergent branches around the reads):
+    //   c < NU : -M[0:NB, NB+c],  U0 = M[NB+a, NB+c]
+    //   c < NY : Jc_b column,     U0 = -Jc_a column        (row JC0 + c - NU of A)
+    //   c = NY : -C_b,            U0 = C_a
+    const bool cu = c < NU, cz = !cu && c < NY;
+    const double* xp = cu ? sM + NB + c : (cz ? sA + (JC0 + c - NU) * NAP : sC);
+    const int xs = cu ? NV : 1;
+    const double xsg = cz ? 1.0 : -1.0;
+    const double* up = cu ? sM + NB * NV + NB + c : (cz ? sA + (JC0 + c - NU) * NAP + NB : sC + NB);
+    const double usg = cz ? -1.0 : 1.0;
     double x[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      double r;
-      if (c < NU) r = -sM[i * NV + NB + c];
-      else if (c < NY) r = sA[(JC0 + c - NU) * NAP + i];
-      else r = -sC[i];
-      x[i] = pinned ? 0.0 : r;
-    }
+    for (int i = 0; i < NB; ++i) x[i] = pinned ? 0.0 : xsg * xp[i * xs];
     // LDL^T of the NB x NB base block (redundantly per lane; NB^3/6 flops)
     double L[NB][NB];
     double dinv[NB];
@@ -474,7 +516,7 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
       for (int j = 0; j <= i; ++j) L[i][j] = sM[i * NV + j];
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      dinv[k] = 1.0 / L[k][k];
+      dinv[k] = recip1(L[k][k]);
 #pragma unroll
       for (int i = k + 1; i < NB; ++i) {          // trailing update with the unscaled column
         const double lik = L[i][k] * dinv[k];
@@ -494,31 +536,40 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     for (int k = NB - 1; k >= 0; --k)
 #pragma unroll
       for (int i = 0; i < k; ++i) x[i] = fma(-L[k][i], x[k], x[i]);
+    if (a_lo == 0) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = x[i];
-    for (int a = 0; a < NU; ++a) {
-      double acc;
-      if (c < NU) acc = sM[(NB + a) * NV + NB + c];
-      else if (c < NY) acc = -sA[(JC0 + c - NU) * NAP + NB + a];
-      else acc = sC[NB + a];
-      if (pinned) acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
-      sU[a * NY1P + c] = acc;
+      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = x[i];
     }
-  } else if (lane < NY1P) {   // padding column of X and U: read by the 2x2 tiles, must be 0
 #pragma unroll
-    for (int i = 0; i < NB; ++i) sX[i * NY1P + lane] = 0.0;
-    for (int a = 0; a < NU; ++a) sU[a * NY1P + lane] = 0.0;
+    for (int t = 0; t < kUStep; ++t) {
+      const int a = a_lo + t;
+      if (a < NU) {
+        double acc = pinned ? 0.0 : usg * up[a * xs];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
+        sU[a * NY1P + c] = acc;
+      }
+    }
+  } else if (c < NY1P) {   // padding column of X and U: read by the 2x2 tiles, must be 0
+    if (a_lo == 0) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < kUStep; ++t)
+      if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = 0.0;
   }
   wave_sync();   // J, M, C dead from here on (R1, R2 get reused)
 
+  STAMP_END(2);
+  STAMP_BEGIN();
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
   // dv = Pm [y;1] with Pm = [X ; (I_nu 0 0)],  T1 = H_dv Pm (+ f_dv in the affine column),
   // Hr = Pm' T1 + 2 (w_tau + w_reg) U'U + 2 w_reg I_z,   g = last column.
   // T1 = H_dv Pm: one 2x2 tile (rows r0, r0+1 x columns c0, c0+1) per lane and round.
   auto t1_base = [&](int r, int c) -> double {
-    return (c < NU) ? sHa[r * NA + NB + c] : ((c == NY) ? sHa[r * NA + NV] : 0.0);
+    const double v = sHa[r * NA + ((c < NU) ? NB + c : NV)];   // read unconditionally
+    return (c < NU || c == NY) ? v : 0.0;
   };
   for (int p = lane; p < D::NBT; p += kWave) {
     const int r0 = 2 * (p / D::NY2), c0 = 2 * (p % D::NY2);
@@ -537,6 +588,8 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     *reinterpret_cast<double2*>(sT1 + (r0 + 1) * NY1P + c0) = make_double2(t10, t11);
   }
   wave_sync();
+  STAMP_END(3);
+  STAMP_BEGIN();
   {
     // Hr | g = Pm' T1 + 2 (w_tau + w_reg) U'U (+ 2 w_reg I_z): one 2x2 tile of the upper
     // triangle per lane and round; each entry (a <= b) accumulates X[r][a] T1[r][b] and
@@ -544,11 +597,13 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
     auto put_hr = [&](int a, int b, double acc) {
+      const int kz = (a >= NU) ? (a - NU) / 3 : 0;
+      const double mk = sMask[kz < NC ? kz : NC - 1];      // read before any branch
       if (b >= NY1 || (a == NY && b == NY)) return;
       if (b < NY) {
         if (a == b && a >= NU) {
           acc += wr2;
-          if (sMask[(a - NU) / 3] == 0.0) acc = 1.0;   // pinned z: identity row
+          if (mk == 0.0) acc = 1.0;   // pinned z: identity row
         }
         sHr[a * NY + b] = acc;
         sHr[b * NY + a] = acc;
@@ -557,13 +612,17 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
       }
     };
     for (int p = lane; p < D::NBH; p += kWave) {
-      const int a0 = 2 * kPairs<D::NY2, false>.a[p], b0 = 2 * kPairs<D::NY2, false>.b[p];
+      int a0, b0;
+      upper_pair<D::NY2>(p, a0, b0);
+      a0 *= 2;
+      b0 *= 2;
       double h[2][2], uu[2][2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          h[i][j] = (a0 + i < NU) ? sT1[(NB + a0 + i) * NY1P + b0 + j] : 0.0;
+          const double t1 = sT1[(NB + ((a0 + i < NU) ? a0 + i : NU - 1)) * NY1P + b0 + j];
+          h[i][j] = (a0 + i < NU) ? t1 : 0.0;
           uu[i][j] = 0.0;
         }
 #pragma unroll
@@ -592,12 +651,16 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   }
   wave_sync();
 
+  STAMP_END(4);
+  STAMP_BEGIN();
   // ---------------- write the reduced QP: workspace [Hr | g | U | X] -------------------------
   double* w = ws + static_cast<size_t>(env) * D::WS;
   for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
   for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
   for (int i = lane; i < NU * NY1P; i += kWave) w[D::W_U + i] = sU[i];
   for (int i = lane; i < NB * NY1P; i += kWave) w[D::W_X + i] = sX[i];
+  STAMP_END(5);
+  STAMP_STORE_SETUP();
 }
 
 // ============================ kernel 2: interior point, 4 env / wave ========================
@@ -1530,5 +1593,11 @@ extern "C" int osc_debug_stamps(unsigned long long* host, int nblocks) {
   if (nblocks > kStampBlocks) nblocks = kStampBlocks;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kStampSlots *
                              nblocks) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+// Same for the setup kernel (one block per env): [nblocks][kStampSlots], slots 0-5 used.
+extern "C" int osc_debug_setup_stamps(unsigned long long* host, int nblocks) {
+  if (nblocks > kStampBlocks) nblocks = kStampBlocks;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_stamps), sizeof(unsigned long long) *
+                             kStampSlots * nblocks) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
 }
 #endif
