@@ -29,6 +29,7 @@ def kernel_ms(s, args, out, reps=10):
 
 
 EPS = [float(a) for a in sys.argv[1:]] or [1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7]
+tau_ref = {}   # tau at the first eps of the list, per workload: the others' tau error against it
 for eps in EPS:
     row = {"eps_mu": eps}
     err = 0.0
@@ -51,7 +52,13 @@ for eps in EPS:
         ms = kernel_ms(s, args, out)
         it = out.iters.cpu().numpy()
         st = out.status.cpu().numpy()
-        row[f"{robot}_{nenv}"] = {"ms": round(ms, 4), "mean_it": round(float(it.mean()), 2),
-                                  "wave_max_it": round(float(it.reshape(-1, 4).max(1).mean()), 2),
-                                  "ok": float((st == 0).mean())}
+        tau = out.tau.cpu().numpy()
+        key = f"{robot}_{nenv}"
+        tau_ref.setdefault(key, tau)
+        ref = tau_ref[key]
+        terr = float((np.abs(tau - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1.0)).max())
+        row[key] = {"ms": round(ms, 4), "mean_it": round(float(it.mean()), 2),
+                    "wave_max_it": round(float(it.reshape(-1, 4).max(1).mean()), 2),
+                    "max_it": int(it.max()), "ok": float((st == 0).mean()),
+                    "tau_err_vs_first": terr}
     print(json.dumps(row), flush=True)

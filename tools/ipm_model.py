@@ -62,6 +62,43 @@ def reduce_qp(model, M, C, J, b, T, mask):
     return Hr, g, np.array(rows), np.array(hs), P, p0
 
 
+def reduce_qp_tau(model, M, C, J, b, T, mask):
+    """Alternative reduction y = (u, z): dv = M^-1 (B u + Jc z - C) from all nv dynamics rows,
+    so the torque bounds are plain bounds on y (no dense U rows)."""
+    qp = build_qp(model, M, C, J, b, T, mask)
+    nv, nu, nc = model.nv, model.nu, model.nc
+    nz, NB = 3 * nc, nv - nu
+    NY = nu + nz
+    n = model.n
+    Jc = contact_jacobian(model, J)
+    pinned = np.repeat(np.asarray(mask) == 0, 3)
+    Jcm = Jc * (~pinned)[None, :]
+    Minv = np.linalg.inv(M)
+    Bm = np.zeros((nv, nu)); Bm[NB:] = np.eye(nu)
+    P = np.zeros((n, NY))
+    p0 = np.zeros(n)
+    P[:nv] = Minv @ np.hstack([Bm, Jcm])
+    p0[:nv] = -Minv @ C
+    P[nv:nv + nu, :nu] = np.eye(nu)
+    P[nv + nu:, nu:] = np.eye(nz)
+    Hr = P.T @ qp.H @ P
+    g = P.T @ (qp.H @ p0 + qp.f)
+    rows, hs = [], []
+    for q in range(nu):
+        r = np.zeros(NY); r[q] = 1.0; rows.append(r); hs.append(model.u_ub[q])
+        r = np.zeros(NY); r[q] = -1.0; rows.append(r); hs.append(-model.u_lb[q])
+    for k in range(nc):
+        if mask[k] == 0:
+            continue
+        zc = nu + 3 * k
+        for sx, sy in ((1, 1), (-1, 1), (1, -1), (-1, -1)):
+            r = np.zeros(NY); r[zc] = sx; r[zc + 1] = sy; r[zc + 2] = -model.mu
+            rows.append(r); hs.append(0.0)
+        r = np.zeros(NY); r[zc + 2] = -1.0; rows.append(r); hs.append(0.0)
+        r = np.zeros(NY); r[zc + 2] = 1.0; rows.append(r); hs.append(BIG_NUMBER * mask[k])
+    return Hr, g, np.array(rows), np.array(hs), P, p0
+
+
 def ldl_factor(K):
     """The kernel's LDL^T: right-looking, Cholesky-infinity guard (pivot <= 1e-13 * original
     diagonal -> 1e128), as ldl_rows in osc_batch.hip."""
@@ -85,6 +122,9 @@ def ldl_solve(F, r):
     L, d = F
     z = sla.solve_triangular(L, r, lower=True, unit_diagonal=True)
     return sla.solve_triangular(L.T, z / d, lower=False, unit_diagonal=True)
+
+
+TRACE = None   # set to a list to record (it, mu, a_aff, a, alpha, sigma) per iteration
 
 
 def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
@@ -256,6 +296,9 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
             if v.startswith("cap"):         # eta <= 1 - c
                 eta = min(eta, 1.0 - float(v[3:]))
         alpha = min(1.0, eta * a)
+        if TRACE is not None:
+            TRACE.append((it, mu, a_aff, a, alpha, sig, float(np.abs(rp).max()),
+                          float(np.abs(rd).max())))
         y, s, lam = y + alpha * dy, s + alpha * ds, lam + alpha * dl
         if rp_c is not None:
             rp_c = (1.0 - alpha) * rp_c
