@@ -142,7 +142,8 @@ struct IpmLayout {
   static constexpr int I_MASK = I_DR + D::NRL * kRow;
   static constexpr int I_TAU = I_MASK + even(NC);
   static constexpr int I_XB = I_TAU + even(NU);
-  static constexpr int IL = I_XB + even(NB);
+  static constexpr int I_DINV = I_XB + even(NB);          // 1/D of the factorization (32)
+  static constexpr int IL = I_DINV + 2 * kRow;
 };
 template <class D>
 constexpr bool hr_fits_lds() {   // four one-wave workgroups per CU, 160 KB of LDS
@@ -741,12 +742,16 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // broadcast by DPP straight into the FMA.  On exit (for slot column j):
 //   c[i], i > j : L[i][j] * D[j]     (column j of L, unscaled)
 //   c[i], i < j : L[j][i] * D[i]     (row j of L, scaled -- left by the symmetric update)
-//   d, dinv     : D[j], 1 / D[j]
-// sdg: original diagonal (Cholesky-infinity test: a pivot below 1e-13 of it becomes 1e128).
+//   dinv0, dinv1: 1 / D[j]
+// thr0, thr1: 1e-13 x the original diagonal (Cholesky-infinity test: a pivot not above it
+// becomes 1e128).  sdinv: 2 x 16 doubles of LDS for this row: every lane writes 1/D_k at step k
+// (one ds_write instead of a lane select), each lane reads its own two back at the end.
+// Slot-1 lanes past N (N < 32) hold a copy of column N-1 (the caller loads jj1 = N-1 there);
+// they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
+// finite, and never a broadcast source.
 template <int N>
-__device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
+__device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
-  dinv0 = dinv1 = 1.0;
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
@@ -756,15 +761,12 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
     const double own = (s == 0) ? c0[k] : c1[k];
     const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
     const double inv = recip1(dk);
-    constexpr unsigned long long kPiv = rows_mask(1u << kl);
-    if constexpr (s == 0) {
-      dinv0 = select_lanes<kPiv>(inv, dinv0);
-    } else {
-      dinv1 = select_lanes<kPiv>(inv, dinv1);
-    }
-    // -L[lane][k] for the lanes still to be eliminated (slot 0: lane > k; slot 1: lane+16 > k)
+    sdinv[k] = inv;
+    // -L[lane][k] for the lanes still to be eliminated (slot 0: lane > k; slot 1: lane+16 > k,
+    // which holds for every slot-1 lane -- padding mirrors included -- while k < 16)
     const double t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(-c0[k] * inv);
-    const double t1 = keep_lanes<rows_mask(lanes_from(k + 1 - kRow, N - 1 - kRow))>(-c1[k] * inv);
+    constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
+    const double t1 = keep_lanes<rows_mask(kT1)>(-c1[k] * inv);
     static_for<k + 1, N>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (s == 0) {
@@ -775,6 +777,9 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N],
       }
     });
   });
+  wave_sync();
+  dinv0 = sdinv[l];
+  dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
 }
 
 // Solve K x = r with the factor above; r0 (var l), r1 (var l+16) in, x out.  Every lane of
@@ -1212,7 +1217,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
-    ldl_rows<NY>(c0, c1, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+    ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
     wave_sync();
     STAMP_END(3);
 

@@ -9,6 +9,7 @@ template <int N>
 __global__ void k_check(const double* K, const double* r, double* x, double* F) {
   const int lane = threadIdx.x, grp = lane / kRow, l = lane % kRow;
   __shared__ double sdg[4][N];
+  __shared__ double sdinv[4][2 * kRow];
   const double* Kg = K + grp * N * N;
   double c0[N], c1[N];
   const int j1 = l + kRow < N ? l + kRow : N - 1;
@@ -20,7 +21,7 @@ __global__ void k_check(const double* K, const double* r, double* x, double* F) 
   if (l + kRow < N) sdg[grp][l + kRow] = Kg[j1 * N + j1];
   __syncthreads();
   double d0, d1;
-  ldl_rows<N>(c0, c1, d0, d1, 1e-13 * Kg[l * N + l], 1e-13 * Kg[j1 * N + j1]);  // d0/d1 = 1/D
+  ldl_rows<N>(c0, c1, sdinv[grp], l, d0, d1, 1e-13 * Kg[l * N + l], 1e-13 * Kg[j1 * N + j1]);  // d0/d1 = 1/D
   for (int i = 0; i < N; ++i) {
     F[grp * N * N + i * N + l] = c0[i];
     if (l + kRow < N) F[grp * N * N + i * N + l + kRow] = c1[i];
