@@ -74,6 +74,15 @@ def cpu_baseline(robot: str, seconds: float, cores: int) -> dict:
                       f"iters/tick); single core alone {rate1:.0f} solves/s"}
 
 
+def baseline_config_tag(args, nenv):
+    """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
+    tags = {("unitree_go2", "standing", "ones", 4096): 1,
+            ("walter_sr", "standing", "ones", 4096): 2,
+            ("walter_sr", "tumbling", "bernoulli", 8192): 3}
+    c = tags.get((args.robot, args.scenario, args.mask, nenv))
+    return f" (BASELINE configs[{c}])" if c is not None else ""
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,7 +176,7 @@ def main() -> None:
             "dtype": "f64",
             "data": "synthetic (seeded post-kinematics M, C, J, b, T, mask; osc_amd.synth)",
             "config": {"workload": f"{args.robot} {args.scenario} mask={args.mask}, "
-                                   f"{nenv} envs per GPU (BASELINE configs[1])",
+                                   f"{nenv} envs per GPU{baseline_config_tag(args, nenv)}",
                        "robot": args.robot, "envs_per_gpu": nenv, "global_envs": total,
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
