@@ -1,0 +1,111 @@
+"""CPU checks of the kinematics oracle (oracle/kinematics.py) against physical identities -- the
+pins that stand in for MuJoCo, which is absent here (parity against it stays unpinned):
+  * Jp qvel / Jr qvel = finite-difference velocity of each site / body orientation,
+  * b = d/dt (J) qvel = finite difference of J qvel along the motion,
+  * 1/2 qvel' M qvel = kinetic energy from finite-difference body velocities,
+  * C(q, 0) = gradient of the gravity potential,
+  * qvel' (C(q, qvel) - C(q, 0)) = 1/2 qvel' Mdot qvel  (energy balance of the velocity terms),
+  * M symmetric positive definite, armature on the diagonal."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "oracle"))
+import kinematics as kin  # noqa: E402
+
+ROBOTS = ["unitree_go2", "walter_sr"]
+EPS = 1e-6
+
+
+def _rot_vee(Rd):
+    """Angle-axis vector of a small rotation matrix."""
+    A = 0.5 * (Rd - Rd.T)
+    return np.array([A[2, 1], A[0, 2], A[1, 0]])
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_sizes_match_the_qp_models(robot):
+    m = kin.load(robot)
+    nv, ns = {"unitree_go2": (18, 5), "walter_sr": (14, 17)}[robot]
+    assert (m.nv, m.ns, m.nq) == (nv, ns, nv + 1)
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_jacobians_match_finite_differences(robot):
+    m = kin.load(robot)
+    rng = np.random.default_rng(11)
+    for _ in range(3):
+        q, v = kin.random_state(m, rng, base_pos_zero=False)
+        M, C, J, b = kin.kinematics(m, q, v)
+        qp, qm = kin.integrate(m, q, v, EPS), kin.integrate(m, q, v, -EPS)
+        vel = (kin.site_positions(m, qp) - kin.site_positions(m, qm)) / (2 * EPS)
+        np.testing.assert_allclose(J[:3 * m.ns].reshape(m.ns, 3, -1) @ v, vel, rtol=0, atol=1e-7)
+        _, Rp, _, _ = kin.forward(m, qp)
+        _, Rm, _, _ = kin.forward(m, qm)
+        for k, s in enumerate(m.sites):
+            w = _rot_vee(Rp[s["body"]] @ Rm[s["body"]].T) / (2 * EPS)
+            np.testing.assert_allclose(J[3 * m.ns + 3 * k:3 * m.ns + 3 * k + 3] @ v, w,
+                                       rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_jdot_qdot_matches_finite_differences(robot):
+    m = kin.load(robot)
+    rng = np.random.default_rng(12)
+    for _ in range(3):
+        q, v = kin.random_state(m, rng)
+        _, _, _, b = kin.kinematics(m, q, v)
+        Jp = kin.kinematics(m, kin.integrate(m, q, v, EPS), v)[2]
+        Jm = kin.kinematics(m, kin.integrate(m, q, v, -EPS), v)[2]
+        np.testing.assert_allclose((Jp - Jm) @ v / (2 * EPS), b, rtol=0,
+                                   atol=1e-6 * (1 + np.abs(b).max()))
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_mass_matrix_is_the_kinetic_energy(robot):
+    m = kin.load(robot)
+    rng = np.random.default_rng(13)
+    for _ in range(3):
+        q, v = kin.random_state(m, rng)
+        M = kin.kinematics(m, q, v)[0]
+        assert np.allclose(M, M.T, atol=1e-14)
+        assert np.linalg.eigvalsh(M).min() > 0
+        qp, qm = kin.integrate(m, q, v, EPS), kin.integrate(m, q, v, -EPS)
+        xp, Rp, _, _ = kin.forward(m, qp)
+        xm, Rm, _, _ = kin.forward(m, qm)
+        _, R0, _, _ = kin.forward(m, q)
+        ke = 0.5 * float(np.sum(m.armature * v * v))
+        for i, bd in enumerate(m.bodies):
+            ip = np.asarray(bd["ipos"])
+            vc = ((xp[i] + Rp[i] @ ip) - (xm[i] + Rm[i] @ ip)) / (2 * EPS)
+            w = _rot_vee(Rp[i] @ Rm[i].T) / (2 * EPS)
+            Iw = R0[i] @ m.Ibody[i] @ R0[i].T
+            ke += 0.5 * (bd["mass"] * vc @ vc + w @ Iw @ w)
+        assert abs(0.5 * v @ M @ v - ke) <= 1e-7 * (1 + ke)
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_bias_gravity_and_energy_balance(robot):
+    m = kin.load(robot)
+    rng = np.random.default_rng(14)
+    for _ in range(3):
+        q, v = kin.random_state(m, rng)
+        M, C, _, _ = kin.kinematics(m, q, v)
+        g = kin.kinematics(m, q, np.zeros(m.nv))[1]
+        # C(q, 0) = dV/dq along every dof direction (integrate = the dof's own motion)
+        grad = np.zeros(m.nv)
+        for i in range(m.nv):
+            e = np.zeros(m.nv)
+            e[i] = 1.0
+            grad[i] = (kin.potential(m, kin.integrate(m, q, e, EPS)) -
+                       kin.potential(m, kin.integrate(m, q, e, -EPS))) / (2 * EPS)
+        np.testing.assert_allclose(g, grad, rtol=0, atol=1e-6 * (1 + np.abs(g).max()))
+        # qvel' c(q, qvel) = 1/2 qvel' Mdot qvel
+        Mp = kin.kinematics(m, kin.integrate(m, q, v, EPS), v)[0]
+        Mm = kin.kinematics(m, kin.integrate(m, q, v, -EPS), v)[0]
+        lhs = v @ (C - g)
+        rhs = 0.5 * v @ ((Mp - Mm) / (2 * EPS)) @ v
+        assert abs(lhs - rhs) <= 1e-6 * (1 + abs(lhs))
