@@ -1,0 +1,900 @@
+// osc_kinematics.hip -- batched floating-base rigid-body kinematics for gfx950 (MI355X): the
+// GPU front end of the OSC solve (C-ABI in include/osc_kinematics.h).
+//
+// Replaces, per environment, what the reference asks MuJoCo for every tick (paths relative to
+// the reference's operational-space-control/):
+//   update_mj_data   unitree_go2/operational_space_controller.h:350-374
+//   update_osc_data  unitree_go2/operational_space_controller.h:376-455
+//     M = mj_fullM (:380), C = qfrc_bias (:383), J = [Jp_0..; Jr_0..] from mj_jac per site
+//     (:401-429), b = [Jpd; Jrd] qvel from mj_jacDot (:430-434).
+//
+// Formulation: spatial vectors in WORLD coordinates about the world origin (Featherstone's
+// CRBA / RNEA without any frame transforms between bodies).  For every body b:
+//   v_b = (w, v_O)      spatial velocity (angular velocity, velocity of the world-origin point)
+//   a_b = (al, a_O)     spatial bias acceleration at zero joint acceleration
+//   I_b = (m, h = m c, I_O)   spatial inertia about the origin; I (w, v) = (I_O w + h x v,
+//                             m v - h x w)
+// A hinge dof has S = (a, p x a) (axis a through anchor p); a free joint's translational dofs
+// are (0, e_k) (world axes) and its rotational dofs (R e_k, x x R e_k) (body axes through the
+// body origin: MuJoCo's body-frame angular qvel).  Since S of a hinge is fixed in its parent,
+// dS/dt = v_parent x S, so a_b = a_p + v_p x (S qd); the free root has a = (0, v x w).
+//   qfrc_bias: f_b = I_b (a_b - (0, g)) + v_b x* I_b v_b, summed over subtrees, C_d = S_d . f.
+//   mj_fullM:  M_ij = S_i . (Ic_{body(j)} S_j) for body(i) an ancestor of body(j) (Ic =
+//              subtree composite inertia), + armature on the diagonal.
+//   mj_jac:    column d of a point x on body k (d an ancestor dof): Jr = S_d.w,
+//              Jp = S_d.v + S_d.w x x.   mj_jacDot qvel: classical acceleration of x at zero
+//              joint acceleration, a_O + al x x + w x (v_O + w x x), and al.
+// The CPU oracle (oracle/kinematics.py) computes the same quantities a different way (COM
+// Jacobians, Kane's method), pinned by finite-difference and energy identities.
+//
+// Mapping: FOUR environments per 64-lane wavefront, one 16-lane row each (the IPM kernel's
+// layout).  Tree recursions run level by level with lane = body (trees are shallow: Go2 4
+// levels, WaLTER 3); the dof, site and dense output stages run with lane = dof / site / output
+// element, so the M and J rows leave as 128-byte coalesced stores.  Per-env state lives in
+// LDS (6.3 KB Go2, 5.1 KB WaLTER), sized at launch from the model.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <new>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include <dlfcn.h>
+
+#include "osc_batch.h"
+#include "osc_kinematics.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kRow = 16;
+constexpr int kEnvPerWave = kWave / kRow;
+constexpr int kBodyStride = 40;   // doubles of per-body LDS state (see the B_* offsets)
+constexpr int kDofStride = 12;    // S (6) | F = Ic S (6)
+
+// per-body LDS state offsets
+constexpr int B_R = 0, B_X = 9, B_W = 12, B_VO = 15, B_AL = 18, B_AO = 21, B_M = 24, B_H = 25,
+              B_IO = 28, B_F = 34;   // IO: xx yy zz xy xz yz;  F: (n, f) total force
+
+// Device-resident model tables (derived on the host from osc_kin_desc).
+struct KinDev {
+  int32_t nbody, nq, nv, nsite, ndepth;
+  int32_t parent[OSC_KIN_MAX_BODIES];
+  int32_t jtype[OSC_KIN_MAX_BODIES];
+  int32_t qadr[OSC_KIN_MAX_BODIES];
+  int32_t dadr[OSC_KIN_MAX_BODIES];
+  int32_t depth[OSC_KIN_MAX_BODIES];
+  int32_t first_child[OSC_KIN_MAX_BODIES];
+  int32_t next_sibling[OSC_KIN_MAX_BODIES];
+  uint32_t anc[OSC_KIN_MAX_BODIES];          // ancestor-or-self body mask
+  int32_t dof_body[OSC_KIN_MAX_DOFS];
+  int32_t site_body[OSC_KIN_MAX_SITES];
+  double gravity[3];
+  double rq[OSC_KIN_MAX_BODIES][9];          // body_quat as a rotation (row-major)
+  double pos[OSC_KIN_MAX_BODIES][3];
+  double axis[OSC_KIN_MAX_BODIES][3];        // unit
+  double jpos[OSC_KIN_MAX_BODIES][3];
+  double arm[OSC_KIN_MAX_BODIES];
+  double mass[OSC_KIN_MAX_BODIES];
+  double ipos[OSC_KIN_MAX_BODIES][3];
+  double ib[OSC_KIN_MAX_BODIES][6];          // body-frame inertia about the COM
+  double site_pos[OSC_KIN_MAX_SITES][3];
+};
+
+constexpr int even(int a) { return (a + 1) & ~1; }
+
+struct EnvLayout {   // per-env LDS layout in doubles
+  int q, body, dof, site, size;
+  __host__ __device__ EnvLayout(int nq, int nv, int nb, int ns) {
+    q = 0;
+    body = even(nq + nv);
+    dof = body + kBodyStride * nb;
+    site = dof + kDofStride * nv;
+    size = even(site + 3 * ns);
+  }
+};
+
+__device__ __forceinline__ void wave_sync() {   // one wavefront per workgroup (osc_batch.hip)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void cross(const double* a, const double* b, double* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// (n, f) = I (w, v) with I = (m, h, IO)
+__device__ __forceinline__ void inertia_mul(double m, const double* h, const double* IO,
+                                            const double* w, const double* v, double* n,
+                                            double* f) {
+  double hv[3], hw[3];
+  cross(h, v, hv);
+  cross(h, w, hw);
+  n[0] = IO[0] * w[0] + IO[3] * w[1] + IO[4] * w[2] + hv[0];
+  n[1] = IO[3] * w[0] + IO[1] * w[1] + IO[5] * w[2] + hv[1];
+  n[2] = IO[4] * w[0] + IO[5] * w[1] + IO[2] * w[2] + hv[2];
+  for (int k = 0; k < 3; ++k) f[k] = m * v[k] - hw[k];
+}
+
+// Forward pass for body b (its parent's state is final): frame, velocity, bias acceleration,
+// spatial inertia and the body's own RNEA force.  Writes the body's LDS state.
+__device__ void body_forward(const KinDev* __restrict__ K, double* E, const EnvLayout& lay,
+                             int b) {
+  double R[9], x[3], w[3], vo[3], al[3], ao[3];
+  const int jt = K->jtype[b];
+  const double* q = E + lay.q;
+  const double* qd = E + lay.q + K->nq;
+  if (jt == OSC_KIN_JOINT_FREE) {
+    const int qa = K->qadr[b], da = K->dadr[b];
+    x[0] = q[qa];
+    x[1] = q[qa + 1];
+    x[2] = q[qa + 2];
+    double qw = q[qa + 3], qx = q[qa + 4], qy = q[qa + 5], qz = q[qa + 6];
+    const double inv = 1.0 / sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+    qw *= inv; qx *= inv; qy *= inv; qz *= inv;
+    R[0] = 1 - 2 * (qy * qy + qz * qz); R[1] = 2 * (qx * qy - qw * qz); R[2] = 2 * (qx * qz + qw * qy);
+    R[3] = 2 * (qx * qy + qw * qz); R[4] = 1 - 2 * (qx * qx + qz * qz); R[5] = 2 * (qy * qz - qw * qx);
+    R[6] = 2 * (qx * qz - qw * qy); R[7] = 2 * (qy * qz + qw * qx); R[8] = 1 - 2 * (qx * qx + qy * qy);
+    const double v[3] = {qd[da], qd[da + 1], qd[da + 2]};
+    const double wl[3] = {qd[da + 3], qd[da + 4], qd[da + 5]};
+    for (int i = 0; i < 3; ++i) w[i] = R[3 * i] * wl[0] + R[3 * i + 1] * wl[1] + R[3 * i + 2] * wl[2];
+    double xw[3];
+    cross(x, w, xw);
+    for (int i = 0; i < 3; ++i) {
+      vo[i] = v[i] + xw[i];     // v_O = v - w x x
+      al[i] = 0.0;
+    }
+    cross(v, w, ao);            // a_O = v x w  (the body origin itself does not accelerate)
+  } else {
+    const int p = K->parent[b];
+    double pR[9], px[3], pw[3], pvo[3], pal[3], pao[3];
+    if (p >= 0) {
+      const double* P = E + lay.body + kBodyStride * p;
+      for (int i = 0; i < 9; ++i) pR[i] = P[B_R + i];
+      for (int i = 0; i < 3; ++i) {
+        px[i] = P[B_X + i]; pw[i] = P[B_W + i]; pvo[i] = P[B_VO + i];
+        pal[i] = P[B_AL + i]; pao[i] = P[B_AO + i];
+      }
+    } else {
+      for (int i = 0; i < 9; ++i) pR[i] = (i % 4 == 0) ? 1.0 : 0.0;
+      for (int i = 0; i < 3; ++i) px[i] = pw[i] = pvo[i] = pal[i] = pao[i] = 0.0;
+    }
+    const double* rq = K->rq[b];
+    const double* bp = K->pos[b];
+    double Rb[9];
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j)
+        Rb[3 * i + j] = pR[3 * i] * rq[j] + pR[3 * i + 1] * rq[3 + j] + pR[3 * i + 2] * rq[6 + j];
+      x[i] = px[i] + pR[3 * i] * bp[0] + pR[3 * i + 1] * bp[1] + pR[3 * i + 2] * bp[2];
+    }
+    if (jt == OSC_KIN_JOINT_HINGE) {
+      const double* u = K->axis[b];
+      const double* jp = K->jpos[b];
+      double anc[3], a[3];
+      for (int i = 0; i < 3; ++i) {
+        anc[i] = x[i] + Rb[3 * i] * jp[0] + Rb[3 * i + 1] * jp[1] + Rb[3 * i + 2] * jp[2];
+        a[i] = Rb[3 * i] * u[0] + Rb[3 * i + 1] * u[1] + Rb[3 * i + 2] * u[2];
+      }
+      double s, c;
+      sincos(q[K->qadr[b]], &s, &c);
+      // Rodrigues in the body frame: Raa = c I + s [u]x + (1 - c) u u'
+      const double t = 1.0 - c;
+      const double Ra[9] = {c + t * u[0] * u[0], t * u[0] * u[1] - s * u[2], t * u[0] * u[2] + s * u[1],
+                            t * u[0] * u[1] + s * u[2], c + t * u[1] * u[1], t * u[1] * u[2] - s * u[0],
+                            t * u[0] * u[2] - s * u[1], t * u[1] * u[2] + s * u[0], c + t * u[2] * u[2]};
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+          R[3 * i + j] = Rb[3 * i] * Ra[j] + Rb[3 * i + 1] * Ra[3 + j] + Rb[3 * i + 2] * Ra[6 + j];
+      for (int i = 0; i < 3; ++i)
+        x[i] = anc[i] - (R[3 * i] * jp[0] + R[3 * i + 1] * jp[1] + R[3 * i + 2] * jp[2]);
+      const double qv = qd[K->dadr[b]];
+      double pa[3], wj[3], vj[3];
+      cross(anc, a, pa);
+      for (int i = 0; i < 3; ++i) {
+        wj[i] = a[i] * qv;
+        vj[i] = pa[i] * qv;
+        w[i] = pw[i] + wj[i];
+        vo[i] = pvo[i] + vj[i];
+      }
+      double c1[3], c2[3], c3[3];
+      cross(pw, wj, c1);
+      cross(pw, vj, c2);
+      cross(pvo, wj, c3);
+      for (int i = 0; i < 3; ++i) {
+        al[i] = pal[i] + c1[i];
+        ao[i] = pao[i] + c2[i] + c3[i];
+      }
+    } else {   // welded to the parent
+      for (int i = 0; i < 9; ++i) R[i] = Rb[i];
+      for (int i = 0; i < 3; ++i) {
+        w[i] = pw[i]; vo[i] = pvo[i]; al[i] = pal[i]; ao[i] = pao[i];
+      }
+    }
+  }
+  // spatial inertia about the world origin: IO = R Ib R' + m (|c|^2 I - c c'), h = m c
+  const double m = K->mass[b];
+  const double* ip = K->ipos[b];
+  const double* ib = K->ib[b];
+  double c[3];
+  for (int i = 0; i < 3; ++i) c[i] = x[i] + R[3 * i] * ip[0] + R[3 * i + 1] * ip[1] + R[3 * i + 2] * ip[2];
+  const double Ibf[9] = {ib[0], ib[3], ib[4], ib[3], ib[1], ib[5], ib[4], ib[5], ib[2]};
+  double RI[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      RI[3 * i + j] = R[3 * i] * Ibf[j] + R[3 * i + 1] * Ibf[3 + j] + R[3 * i + 2] * Ibf[6 + j];
+  auto rir = [&](int i, int j) {
+    return RI[3 * i] * R[3 * j] + RI[3 * i + 1] * R[3 * j + 1] + RI[3 * i + 2] * R[3 * j + 2];
+  };
+  const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+  double IO[6], h[3];
+  IO[0] = rir(0, 0) + m * (cc - c[0] * c[0]);
+  IO[1] = rir(1, 1) + m * (cc - c[1] * c[1]);
+  IO[2] = rir(2, 2) + m * (cc - c[2] * c[2]);
+  IO[3] = rir(0, 1) - m * c[0] * c[1];
+  IO[4] = rir(0, 2) - m * c[0] * c[2];
+  IO[5] = rir(1, 2) - m * c[1] * c[2];
+  for (int i = 0; i < 3; ++i) h[i] = m * c[i];
+  // own RNEA force: f = I (al, a_O - g) + v x* (I v)
+  double ag[3];
+  for (int i = 0; i < 3; ++i) ag[i] = ao[i] - K->gravity[i];
+  double n1[3], f1[3], ln[3], lf[3];
+  inertia_mul(m, h, IO, al, ag, n1, f1);
+  inertia_mul(m, h, IO, w, vo, ln, lf);
+  double t1[3], t2[3], t3[3];
+  cross(w, ln, t1);
+  cross(vo, lf, t2);
+  cross(w, lf, t3);
+  double* B = E + lay.body + kBodyStride * b;
+  for (int i = 0; i < 9; ++i) B[B_R + i] = R[i];
+  for (int i = 0; i < 3; ++i) {
+    B[B_X + i] = x[i]; B[B_W + i] = w[i]; B[B_VO + i] = vo[i];
+    B[B_AL + i] = al[i]; B[B_AO + i] = ao[i]; B[B_H + i] = h[i];
+    B[B_F + i] = n1[i] + t1[i] + t2[i];
+    B[B_F + 3 + i] = f1[i] + t3[i];
+  }
+  B[B_M] = m;
+  for (int i = 0; i < 6; ++i) B[B_IO + i] = IO[i];
+}
+
+__global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
+    const KinDev* __restrict__ K, int nenv, const double* __restrict__ qpos,
+    const double* __restrict__ qvel, double* __restrict__ gM, double* __restrict__ gC,
+    double* __restrict__ gJ, double* __restrict__ gb, double* __restrict__ gx) {
+  extern __shared__ __attribute__((aligned(16))) double kin_sm[];
+  const int lane = threadIdx.x;
+  const int row = lane / kRow, l = lane % kRow;
+  const int env_raw = blockIdx.x * kEnvPerWave + row;
+  const bool valid = env_raw < nenv;
+  const int env = valid ? env_raw : nenv - 1;   // tail rows recompute the last env, store nothing
+  const int nq = K->nq, nv = K->nv, nb = K->nbody, ns = K->nsite, nd = K->ndepth;
+  const EnvLayout lay(nq, nv, nb, ns);
+  double* E = kin_sm + row * lay.size;
+
+  // ---- stage 0: qpos | qvel -> LDS --------------------------------------------------------
+  for (int i = l; i < nq; i += kRow) E[lay.q + i] = qpos[static_cast<size_t>(env) * nq + i];
+  for (int i = l; i < nv; i += kRow) E[lay.q + nq + i] = qvel[static_cast<size_t>(env) * nv + i];
+  wave_sync();
+
+  // ---- stage 1: forward pass, level by level (lane = body) --------------------------------
+  const int my_depth = (l < nb) ? K->depth[l] : -1;
+  for (int L = 0; L < nd; ++L) {
+    if (my_depth == L) body_forward(K, E, lay, l);
+    wave_sync();
+  }
+
+  // ---- stage 2: backward pass: subtree composite inertia and force ------------------------
+  for (int L = nd - 2; L >= 0; --L) {
+    if (my_depth == L) {
+      double* B = E + lay.body + kBodyStride * l;
+      double acc[10 + 6];
+      for (int i = 0; i < 10; ++i) acc[i] = B[B_M + i];
+      for (int i = 0; i < 6; ++i) acc[10 + i] = B[B_F + i];
+      for (int ch = K->first_child[l]; ch >= 0; ch = K->next_sibling[ch]) {
+        const double* Cb = E + lay.body + kBodyStride * ch;
+        for (int i = 0; i < 10; ++i) acc[i] += Cb[B_M + i];
+        for (int i = 0; i < 6; ++i) acc[10 + i] += Cb[B_F + i];
+      }
+      for (int i = 0; i < 10; ++i) B[B_M + i] = acc[i];
+      for (int i = 0; i < 6; ++i) B[B_F + i] = acc[10 + i];
+    }
+    wave_sync();
+  }
+
+  // ---- stage 3: dofs (lane = dof): motion subspace S, F = Ic S, C = S . f -----------------
+  for (int d = l; d < nv; d += kRow) {
+    const int bb = K->dof_body[d];
+    const double* B = E + lay.body + kBodyStride * bb;
+    double S[6];
+    const int k = d - K->dadr[bb];
+    if (K->jtype[bb] == OSC_KIN_JOINT_FREE) {
+      if (k < 3) {
+        S[0] = S[1] = S[2] = 0.0;
+        for (int i = 0; i < 3; ++i) S[3 + i] = (i == k) ? 1.0 : 0.0;
+      } else {
+        const double a[3] = {B[B_R + k - 3], B[B_R + 3 + k - 3], B[B_R + 6 + k - 3]};
+        const double xo[3] = {B[B_X], B[B_X + 1], B[B_X + 2]};
+        S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
+        cross(xo, a, S + 3);
+      }
+    } else {   // hinge: the axis is invariant under its own rotation, so a = R u
+      const double* u = K->axis[bb];
+      const double* jp = K->jpos[bb];
+      double a[3], pa[3];
+      for (int i = 0; i < 3; ++i) {
+        a[i] = B[B_R + 3 * i] * u[0] + B[B_R + 3 * i + 1] * u[1] + B[B_R + 3 * i + 2] * u[2];
+        pa[i] = B[B_X + i] + B[B_R + 3 * i] * jp[0] + B[B_R + 3 * i + 1] * jp[1] +
+                B[B_R + 3 * i + 2] * jp[2];
+      }
+      S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
+      cross(pa, a, S + 3);
+    }
+    double F[6];
+    inertia_mul(B[B_M], B + B_H, B + B_IO, S, S + 3, F, F + 3);
+    double* Dd = E + lay.dof + kDofStride * d;
+    for (int i = 0; i < 6; ++i) {
+      Dd[i] = S[i];
+      Dd[6 + i] = F[i];
+    }
+    double cd = 0.0;
+    for (int i = 0; i < 6; ++i) cd = fma(S[i], B[B_F + i], cd);
+    if (valid) gC[static_cast<size_t>(env) * nv + d] = cd;
+  }
+
+  // ---- stage 4: sites (lane = site): world position, J-dot qvel ---------------------------
+  for (int k = l; k < ns; k += kRow) {
+    const int bb = K->site_body[k];
+    const double* B = E + lay.body + kBodyStride * bb;
+    const double* sp = K->site_pos[k];
+    double xk[3];
+    for (int i = 0; i < 3; ++i)
+      xk[i] = B[B_X + i] + B[B_R + 3 * i] * sp[0] + B[B_R + 3 * i + 1] * sp[1] +
+              B[B_R + 3 * i + 2] * sp[2];
+    double* Xs = E + lay.site + 3 * k;
+    for (int i = 0; i < 3; ++i) Xs[i] = xk[i];
+    const double w[3] = {B[B_W], B[B_W + 1], B[B_W + 2]};
+    const double al[3] = {B[B_AL], B[B_AL + 1], B[B_AL + 2]};
+    double wx[3], alx[3], vx[3], wvx[3];
+    cross(w, xk, wx);
+    cross(al, xk, alx);
+    for (int i = 0; i < 3; ++i) vx[i] = B[B_VO + i] + wx[i];
+    cross(w, vx, wvx);
+    if (valid) {
+      double* bo = gb + static_cast<size_t>(env) * 6 * ns;
+      for (int i = 0; i < 3; ++i) {
+        bo[3 * k + i] = B[B_AO + i] + alx[i] + wvx[i];
+        bo[3 * ns + 3 * k + i] = al[i];
+      }
+      if (gx) {
+        for (int i = 0; i < 3; ++i) gx[(static_cast<size_t>(env) * ns + k) * 3 + i] = xk[i];
+      }
+    }
+  }
+  wave_sync();
+
+  // ---- stage 5: M (lane = element, row-major): M_ij = S_lo . F_hi if related --------------
+  {
+    double* Mo = gM + static_cast<size_t>(env) * nv * nv;
+    int i = 0, j = l;
+    while (j >= nv) { j -= nv; ++i; }
+    for (int e = l; e < nv * nv; e += kRow) {
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int blo = K->dof_body[lo], bhi = K->dof_body[hi];
+      double v = 0.0;
+      if ((K->anc[bhi] >> blo) & 1u) {
+        const double* Sl = E + lay.dof + kDofStride * lo;
+        const double* Fh = E + lay.dof + kDofStride * hi + 6;
+        for (int t = 0; t < 6; ++t) v = fma(Sl[t], Fh[t], v);
+        if (i == j) v += K->arm[blo];
+      }
+      if (valid) Mo[e] = v;
+      j += kRow;
+      while (j >= nv) { j -= nv; ++i; }
+    }
+  }
+
+  // ---- stage 6: J (lane = element, row-major over [Jp rows; Jr rows]) ---------------------
+  {
+    double* Jo = gJ + static_cast<size_t>(env) * 6 * ns * nv;
+    const int nrow = 6 * ns;
+    int r = 0, c = l;
+    while (c >= nv) { c -= nv; ++r; }
+    for (int e = l; e < nrow * nv; e += kRow) {
+      const bool rot = r >= 3 * ns;
+      const int rr = rot ? r - 3 * ns : r;
+      const int k = rr / 3, comp = rr - 3 * k;
+      const int bk = K->site_body[k], bc = K->dof_body[c];
+      double v = 0.0;
+      if ((K->anc[bk] >> bc) & 1u) {
+        const double* S = E + lay.dof + kDofStride * c;
+        if (rot) {
+          v = S[comp];
+        } else {
+          const double* xk = E + lay.site + 3 * k;
+          const int c1 = comp == 2 ? 0 : comp + 1, c2 = comp == 0 ? 2 : comp - 1;
+          v = S[3 + comp] + (S[c1] * xk[c2] - S[c2] * xk[c1]);
+        }
+      }
+      if (valid) Jo[e] = v;
+      c += kRow;
+      while (c >= nv) { c -= nv; ++r; }
+    }
+  }
+}
+
+constexpr int kPackBlock = 256;
+
+// update_mj_data's qpos / qvel packing for a batch of States (osc.h:357-361).
+__global__ __launch_bounds__(kPackBlock) void state_to_qpos_kernel(
+    int nenv, int nu, const double* __restrict__ rot, const double* __restrict__ lin,
+    const double* __restrict__ ang, const double* __restrict__ mpos,
+    const double* __restrict__ mvel, double* __restrict__ qpos, double* __restrict__ qvel) {
+  const int nq = 7 + nu, nvv = 6 + nu;
+  const long long total = static_cast<long long>(nenv) * (nq + nvv);
+  for (long long t = static_cast<long long>(blockIdx.x) * kPackBlock + threadIdx.x; t < total;
+       t += static_cast<long long>(gridDim.x) * kPackBlock) {
+    const long long e = t / (nq + nvv);
+    const int i = static_cast<int>(t - e * (nq + nvv));
+    if (i < nq) {
+      double v;
+      if (i < 3) v = 0.0;                       // base position forced to zero (osc.h:358-359)
+      else if (i < 7) v = rot[e * 4 + (i - 3)];
+      else v = mpos[e * nu + (i - 7)];
+      qpos[e * nq + i] = v;
+    } else {
+      const int k = i - nq;
+      double v;
+      if (k < 3) v = lin[e * 3 + k];
+      else if (k < 6) v = ang[e * 3 + (k - 3)];
+      else v = mvel[e * nu + (k - 6)];
+      qvel[e * nvv + k] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+
+void quat_to_mat(const double* q, double* R) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  const double n = std::sqrt(w * w + x * x + y * y + z * z);
+  w /= n; x /= n; y /= n; z /= n;
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+int build_tables(const osc_kin_desc& d, KinDev* k) {
+  std::memset(k, 0, sizeof(*k));
+  if (d.nbody < 1 || d.nbody > OSC_KIN_MAX_BODIES || d.nsite < 1 || d.nsite > OSC_KIN_MAX_SITES)
+    return OSC_ERR_INVALID_ARGUMENT;
+  int nq = 0, nv = 0, ndepth = 0;
+  for (int b = 0; b < d.nbody; ++b) {
+    const int p = d.parent[b];
+    if (p < -1 || p >= b) return OSC_ERR_INVALID_ARGUMENT;   // parents first (MuJoCo order)
+    const int jt = d.jnt_type[b];
+    if (jt != OSC_KIN_JOINT_NONE && jt != OSC_KIN_JOINT_FREE && jt != OSC_KIN_JOINT_HINGE)
+      return OSC_ERR_INVALID_ARGUMENT;
+    if (jt == OSC_KIN_JOINT_FREE && p != -1) return OSC_ERR_INVALID_ARGUMENT;
+    if (!(d.mass[b] >= 0.0) || !(d.armature[b] >= 0.0)) return OSC_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < 3; ++i)
+      if (!(d.inertia[b][i] >= 0.0)) return OSC_ERR_INVALID_ARGUMENT;
+    const double qn = std::sqrt(d.quat[b][0] * d.quat[b][0] + d.quat[b][1] * d.quat[b][1] +
+                                d.quat[b][2] * d.quat[b][2] + d.quat[b][3] * d.quat[b][3]);
+    const double in = std::sqrt(d.iquat[b][0] * d.iquat[b][0] + d.iquat[b][1] * d.iquat[b][1] +
+                                d.iquat[b][2] * d.iquat[b][2] + d.iquat[b][3] * d.iquat[b][3]);
+    if (!(qn > 0.0) || !(in > 0.0)) return OSC_ERR_INVALID_ARGUMENT;
+    k->parent[b] = p;
+    k->jtype[b] = jt;
+    k->qadr[b] = nq;
+    k->dadr[b] = nv;
+    k->depth[b] = p < 0 ? 0 : k->depth[p] + 1;
+    ndepth = std::max(ndepth, k->depth[b] + 1);
+    k->anc[b] = (p < 0 ? 0u : k->anc[p]) | (1u << b);
+    k->first_child[b] = -1;
+    k->next_sibling[b] = -1;
+    int ndof = 0;
+    if (jt == OSC_KIN_JOINT_FREE) {
+      nq += 7;
+      ndof = 6;
+    } else if (jt == OSC_KIN_JOINT_HINGE) {
+      nq += 1;
+      ndof = 1;
+      const double an = std::sqrt(d.axis[b][0] * d.axis[b][0] + d.axis[b][1] * d.axis[b][1] +
+                                  d.axis[b][2] * d.axis[b][2]);
+      if (!(an > 0.0)) return OSC_ERR_INVALID_ARGUMENT;
+      for (int i = 0; i < 3; ++i) k->axis[b][i] = d.axis[b][i] / an;
+    }
+    if (nv + ndof > OSC_KIN_MAX_DOFS) return OSC_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < ndof; ++i) k->dof_body[nv + i] = b;
+    nv += ndof;
+    quat_to_mat(d.quat[b], k->rq[b]);
+    double Ri[9];
+    quat_to_mat(d.iquat[b], Ri);
+    double Ib[9];   // Ri diag(I) Ri'
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < 3; ++t) s += Ri[3 * i + t] * d.inertia[b][t] * Ri[3 * j + t];
+        Ib[3 * i + j] = s;
+      }
+    k->ib[b][0] = Ib[0]; k->ib[b][1] = Ib[4]; k->ib[b][2] = Ib[8];
+    k->ib[b][3] = Ib[1]; k->ib[b][4] = Ib[2]; k->ib[b][5] = Ib[5];
+    for (int i = 0; i < 3; ++i) {
+      k->pos[b][i] = d.pos[b][i];
+      k->jpos[b][i] = d.jnt_pos[b][i];
+      k->ipos[b][i] = d.ipos[b][i];
+    }
+    k->arm[b] = d.armature[b];
+    k->mass[b] = d.mass[b];
+  }
+  if (nv < 1) return OSC_ERR_INVALID_ARGUMENT;
+  // child lists in body order (fixed summation order: deterministic results)
+  for (int b = d.nbody - 1; b >= 0; --b) {
+    const int p = d.parent[b];
+    if (p >= 0) {
+      k->next_sibling[b] = k->first_child[p];
+      k->first_child[p] = b;
+    }
+  }
+  for (int s = 0; s < d.nsite; ++s) {
+    if (d.site_body[s] < 0 || d.site_body[s] >= d.nbody) return OSC_ERR_INVALID_ARGUMENT;
+    k->site_body[s] = d.site_body[s];
+    for (int i = 0; i < 3; ++i) k->site_pos[s][i] = d.site_pos[s][i];
+  }
+  for (int i = 0; i < 3; ++i) k->gravity[i] = d.gravity[i];
+  k->nbody = d.nbody;
+  k->nq = nq;
+  k->nv = nv;
+  k->nsite = d.nsite;
+  k->ndepth = ndepth;
+  return OSC_OK;
+}
+
+// ---- minimal JSON reader for the <robot>_kinematics.json schema ----------------------------
+struct JVal {
+  enum Kind { NUL, NUM, STR, ARR, OBJ, BOOL } kind = NUL;
+  double num = 0.0;
+  std::string str;
+  std::vector<JVal> arr;
+  std::vector<std::pair<std::string, JVal>> obj;
+  const JVal* get(const char* key) const {
+    for (const auto& kv : obj)
+      if (kv.first == key) return &kv.second;
+    return nullptr;
+  }
+};
+
+struct JParser {
+  const std::string& s;
+  size_t i = 0;
+  explicit JParser(const std::string& src) : s(src) {}
+  void ws() {
+    while (i < s.size() && (s[i] == ' ' || s[i] == '\n' || s[i] == '\t' || s[i] == '\r')) ++i;
+  }
+  bool str(std::string* out) {
+    if (i >= s.size() || s[i] != '"') return false;
+    ++i;
+    out->clear();
+    while (i < s.size() && s[i] != '"') {
+      if (s[i] == '\\' && i + 1 < s.size()) ++i;
+      out->push_back(s[i++]);
+    }
+    if (i >= s.size()) return false;
+    ++i;
+    return true;
+  }
+  bool value(JVal* v, int depth = 0) {
+    if (depth > 32) return false;
+    ws();
+    if (i >= s.size()) return false;
+    const char ch = s[i];
+    if (ch == '{') {
+      v->kind = JVal::OBJ;
+      ++i;
+      ws();
+      if (i < s.size() && s[i] == '}') { ++i; return true; }
+      while (true) {
+        ws();
+        std::string key;
+        if (!str(&key)) return false;
+        ws();
+        if (i >= s.size() || s[i] != ':') return false;
+        ++i;
+        JVal child;
+        if (!value(&child, depth + 1)) return false;
+        v->obj.emplace_back(key, std::move(child));
+        ws();
+        if (i < s.size() && s[i] == ',') { ++i; continue; }
+        if (i < s.size() && s[i] == '}') { ++i; return true; }
+        return false;
+      }
+    }
+    if (ch == '[') {
+      v->kind = JVal::ARR;
+      ++i;
+      ws();
+      if (i < s.size() && s[i] == ']') { ++i; return true; }
+      while (true) {
+        JVal child;
+        if (!value(&child, depth + 1)) return false;
+        v->arr.push_back(std::move(child));
+        ws();
+        if (i < s.size() && s[i] == ',') { ++i; continue; }
+        if (i < s.size() && s[i] == ']') { ++i; return true; }
+        return false;
+      }
+    }
+    if (ch == '"') {
+      v->kind = JVal::STR;
+      return str(&v->str);
+    }
+    if (s.compare(i, 4, "true") == 0) { v->kind = JVal::BOOL; v->num = 1; i += 4; return true; }
+    if (s.compare(i, 5, "false") == 0) { v->kind = JVal::BOOL; i += 5; return true; }
+    if (s.compare(i, 4, "null") == 0) { v->kind = JVal::NUL; i += 4; return true; }
+    const char* start = s.c_str() + i;
+    char* end = nullptr;
+    v->num = std::strtod(start, &end);
+    if (end == start) return false;
+    v->kind = JVal::NUM;
+    i += static_cast<size_t>(end - start);
+    return true;
+  }
+};
+
+bool jnums(const JVal* v, double* out, size_t n) {
+  if (!v || v->kind != JVal::ARR || v->arr.size() != n) return false;
+  for (size_t k = 0; k < n; ++k) {
+    if (v->arr[k].kind != JVal::NUM) return false;
+    out[k] = v->arr[k].num;
+  }
+  return true;
+}
+
+bool jnum(const JVal* v, double* out) {
+  if (!v || v->kind != JVal::NUM) return false;
+  *out = v->num;
+  return true;
+}
+
+std::string kin_library_dir() {
+  Dl_info info;
+  if (dladdr(reinterpret_cast<void*>(&osc_kin_desc_from_json), &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    size_t s = p.rfind('/');
+    if (s != std::string::npos) return p.substr(0, s);
+  }
+  return ".";
+}
+
+}  // namespace
+
+struct osc_kin_model {
+  osc_kin_desc desc;
+  KinDev host;
+  KinDev* dev;
+  int device;
+};
+
+extern "C" int osc_kin_desc_from_json(const char* robot, const char* json_path,
+                                      osc_kin_desc* desc) {
+  if (!desc || (!robot && !json_path)) return OSC_ERR_INVALID_ARGUMENT;
+  const std::string path = json_path ? std::string(json_path)
+                                     : kin_library_dir() + "/../config/" + robot +
+                                           "_kinematics.json";
+  std::ifstream in(path);
+  if (!in) return OSC_ERR_IO;
+  std::stringstream ss;
+  ss << in.rdbuf();
+  const std::string text = ss.str();
+  JVal root;
+  JParser p(text);
+  if (!p.value(&root) || root.kind != JVal::OBJ) {
+    std::fprintf(stderr, "osc_kin_desc_from_json: %s: malformed JSON\n", path.c_str());
+    return OSC_ERR_IO;
+  }
+  std::memset(desc, 0, sizeof(*desc));
+  const JVal* bodies = root.get("bodies");
+  const JVal* sites = root.get("sites");
+  if (!bodies || bodies->kind != JVal::ARR || !sites || sites->kind != JVal::ARR ||
+      !jnums(root.get("gravity"), desc->gravity, 3))
+    return OSC_ERR_IO;
+  if (bodies->arr.size() > OSC_KIN_MAX_BODIES || sites->arr.size() > OSC_KIN_MAX_SITES)
+    return OSC_ERR_INVALID_ARGUMENT;
+  desc->nbody = static_cast<int32_t>(bodies->arr.size());
+  desc->nsite = static_cast<int32_t>(sites->arr.size());
+  for (int b = 0; b < desc->nbody; ++b) {
+    const JVal& B = bodies->arr[b];
+    double parent = 0.0;
+    const JVal* jt = B.get("joint");
+    if (!jnum(B.get("parent"), &parent) || !jt || jt->kind != JVal::STR ||
+        !jnums(B.get("pos"), desc->pos[b], 3) || !jnums(B.get("quat"), desc->quat[b], 4) ||
+        !jnum(B.get("mass"), &desc->mass[b]) || !jnums(B.get("ipos"), desc->ipos[b], 3) ||
+        !jnums(B.get("iquat"), desc->iquat[b], 4) ||
+        !jnums(B.get("diaginertia"), desc->inertia[b], 3))
+      return OSC_ERR_IO;
+    desc->parent[b] = static_cast<int32_t>(parent);
+    if (jt->str == "free") desc->jnt_type[b] = OSC_KIN_JOINT_FREE;
+    else if (jt->str == "hinge") desc->jnt_type[b] = OSC_KIN_JOINT_HINGE;
+    else if (jt->str == "none") desc->jnt_type[b] = OSC_KIN_JOINT_NONE;
+    else return OSC_ERR_IO;
+    if (B.get("axis") && !jnums(B.get("axis"), desc->axis[b], 3)) return OSC_ERR_IO;
+    if (B.get("jnt_pos") && !jnums(B.get("jnt_pos"), desc->jnt_pos[b], 3)) return OSC_ERR_IO;
+    if (B.get("armature") && !jnum(B.get("armature"), &desc->armature[b])) return OSC_ERR_IO;
+  }
+  for (int s = 0; s < desc->nsite; ++s) {
+    const JVal& S = sites->arr[s];
+    double body = 0.0;
+    if (!jnum(S.get("body"), &body) || !jnums(S.get("pos"), desc->site_pos[s], 3))
+      return OSC_ERR_IO;
+    desc->site_body[s] = static_cast<int32_t>(body);
+  }
+  return OSC_OK;
+}
+
+extern "C" int osc_kin_model_create(const osc_kin_desc* desc, osc_kin_model** out) {
+  if (!desc || !out) return OSC_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  osc_kin_model* m = new (std::nothrow) osc_kin_model;
+  if (!m) return OSC_ERR_DEVICE;
+  const int rc = build_tables(*desc, &m->host);
+  if (rc != OSC_OK) {
+    delete m;
+    return rc;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    delete m;
+    return OSC_ERR_NO_DEVICE;
+  }
+  m->desc = *desc;
+  m->dev = nullptr;
+  (void)hipGetDevice(&m->device);
+  if (hipMalloc(&m->dev, sizeof(KinDev)) != hipSuccess ||
+      hipMemcpy(m->dev, &m->host, sizeof(KinDev), hipMemcpyHostToDevice) != hipSuccess) {
+    if (m->dev) (void)hipFree(m->dev);
+    delete m;
+    return OSC_ERR_DEVICE;
+  }
+  *out = m;
+  return OSC_OK;
+}
+
+extern "C" int osc_kin_model_create_from_json(const char* robot, const char* json_path,
+                                              osc_kin_model** out) {
+  osc_kin_desc d;
+  const int rc = osc_kin_desc_from_json(robot, json_path, &d);
+  if (rc != OSC_OK) return rc;
+  return osc_kin_model_create(&d, out);
+}
+
+extern "C" int osc_kin_model_destroy(osc_kin_model* model) {
+  if (!model) return OSC_ERR_INVALID_ARGUMENT;
+  if (model->dev) (void)hipFree(model->dev);
+  delete model;
+  return OSC_OK;
+}
+
+extern "C" int osc_kin_model_dims(const osc_kin_model* model, int32_t* nq, int32_t* nv,
+                                  int32_t* nsite) {
+  if (!model) return OSC_ERR_INVALID_ARGUMENT;
+  if (nq) *nq = model->host.nq;
+  if (nv) *nv = model->host.nv;
+  if (nsite) *nsite = model->host.nsite;
+  return OSC_OK;
+}
+
+extern "C" int osc_batch_kinematics(const osc_kin_model* model, int32_t nenv, const double* qpos,
+                                    const double* qvel, double* M, double* C, double* J,
+                                    double* b, double* site_xpos, void* stream) {
+  if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+  if (nenv == 0) return OSC_OK;
+  if (!qpos || !qvel || !M || !C || !J || !b) return OSC_ERR_INVALID_ARGUMENT;
+  const KinDev& k = model->host;
+  const EnvLayout lay(k.nq, k.nv, k.nbody, k.nsite);
+  const size_t lds = sizeof(double) * static_cast<size_t>(lay.size) * kEnvPerWave;
+  const unsigned nblk = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
+  hipLaunchKernelGGL(osc_kinematics_kernel, dim3(nblk), dim3(kWave), lds,
+                     static_cast<hipStream_t>(stream), model->dev, nenv, qpos, qvel, M, C, J, b,
+                     site_xpos);
+  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+
+extern "C" int osc_state_to_qpos(int32_t nenv, int32_t nu, const double* body_rotation,
+                                 const double* linear_body_velocity,
+                                 const double* angular_body_velocity,
+                                 const double* motor_position, const double* motor_velocity,
+                                 double* qpos, double* qvel, void* stream) {
+  if (nenv < 0 || nu < 0) return OSC_ERR_INVALID_ARGUMENT;
+  if (nenv == 0) return OSC_OK;
+  if (!body_rotation || !linear_body_velocity || !angular_body_velocity || !qpos || !qvel ||
+      (nu > 0 && (!motor_position || !motor_velocity)))
+    return OSC_ERR_INVALID_ARGUMENT;
+  const long long total = static_cast<long long>(nenv) * (13 + 2 * nu);
+  const unsigned nblk = static_cast<unsigned>(std::min<long long>((total + kPackBlock - 1) /
+                                                                  kPackBlock, 4096));
+  hipLaunchKernelGGL(state_to_qpos_kernel, dim3(nblk), dim3(kPackBlock), 0,
+                     static_cast<hipStream_t>(stream), nenv, nu, body_rotation,
+                     linear_body_velocity, angular_body_velocity, motor_position, motor_velocity,
+                     qpos, qvel);
+  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+
+namespace {
+
+size_t align256(size_t n) { return (n + 255) & ~static_cast<size_t>(255); }
+
+struct QposWorkspace {   // [M | C | J | b | reduced-QP workspace], each section 256-B aligned
+  size_t m, c, j, b, ws, ws_bytes, total;
+  QposWorkspace(const osc_model* model, const KinDev& k, int32_t nenv) {
+    const size_t n = static_cast<size_t>(nenv);
+    m = 0;
+    c = m + align256(sizeof(double) * n * k.nv * k.nv);
+    j = c + align256(sizeof(double) * n * k.nv);
+    b = j + align256(sizeof(double) * n * 6 * k.nsite * k.nv);
+    ws = b + align256(sizeof(double) * n * 6 * k.nsite);
+    ws_bytes = 0;
+    osc_workspace_bytes(model, nenv, &ws_bytes);
+    total = ws + align256(ws_bytes);
+  }
+};
+
+int check_pair(const osc_model* model, const osc_kin_model* kin) {
+  if (!model || !kin) return OSC_ERR_INVALID_ARGUMENT;
+  osc_model_desc d;
+  if (osc_model_get_desc(model, &d) != OSC_OK) return OSC_ERR_INVALID_ARGUMENT;
+  if (d.nv != kin->host.nv || d.ns != kin->host.nsite) return OSC_ERR_INVALID_ARGUMENT;
+  return OSC_OK;
+}
+
+}  // namespace
+
+extern "C" int osc_qpos_workspace_bytes(const osc_model* model, const osc_kin_model* kin,
+                                        int32_t nenv, size_t* bytes) {
+  if (!bytes || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+  const int rc = check_pair(model, kin);
+  if (rc != OSC_OK) return rc;
+  *bytes = QposWorkspace(model, kin->host, nenv).total;
+  return OSC_OK;
+}
+
+extern "C" int osc_batch_solve_qpos(const osc_model* model, const osc_kin_model* kin,
+                                    int32_t nenv, const double* qpos, const double* qvel,
+                                    const double* T, const double* contact_mask, double* tau,
+                                    double* x, int32_t* status, int32_t* iters, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  int rc = check_pair(model, kin);
+  if (rc != OSC_OK) return rc;
+  if (nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+  if (nenv == 0) return OSC_OK;
+  if ((reinterpret_cast<uintptr_t>(workspace) & 15u) != 0) return OSC_ERR_INVALID_ARGUMENT;
+  const QposWorkspace L(model, kin->host, nenv);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* base = static_cast<char*>(workspace);
+  bool owned = false;
+  if (base == nullptr) {
+    if (hipMallocAsync(reinterpret_cast<void**>(&base), L.total, s) != hipSuccess)
+      return OSC_ERR_DEVICE;
+    owned = true;
+  } else if (workspace_bytes < L.total) {
+    return OSC_ERR_INVALID_ARGUMENT;
+  }
+  double* M = reinterpret_cast<double*>(base + L.m);
+  double* C = reinterpret_cast<double*>(base + L.c);
+  double* J = reinterpret_cast<double*>(base + L.j);
+  double* b = reinterpret_cast<double*>(base + L.b);
+  rc = osc_batch_kinematics(kin, nenv, qpos, qvel, M, C, J, b, nullptr, stream);
+  if (rc == OSC_OK)
+    rc = osc_batch_solve(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters,
+                         base + L.ws, L.ws_bytes, stream);
+  if (owned) (void)hipFreeAsync(base, s);
+  return rc;
+}

@@ -23,7 +23,16 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
                     "osc_batch_solve", "osc_batch_assemble", "osc_batch_solve_assembled",
                     "osc_status_string", "osc_abi_version",
-                    "osc_pd_base_targets", "osc_contact_mask_from_contacts")
+                    "osc_pd_base_targets", "osc_contact_mask_from_contacts",
+                    "osc_kin_desc_from_json", "osc_kin_model_create",
+                    "osc_kin_model_create_from_json", "osc_kin_model_destroy",
+                    "osc_kin_model_dims", "osc_batch_kinematics", "osc_state_to_qpos",
+                    "osc_qpos_workspace_bytes", "osc_batch_solve_qpos")
+
+OSC_KIN_MAX_BODIES = 16
+OSC_KIN_MAX_DOFS = 32
+OSC_KIN_MAX_SITES = 32
+JOINT_NONE, JOINT_FREE, JOINT_HINGE = -1, 0, 3     # MuJoCo's mjtJoint values
 
 
 class OscModelDesc(ctypes.Structure):
@@ -39,6 +48,24 @@ class OscModelDesc(ctypes.Structure):
         ("infinity", ctypes.c_double),
         ("eps_mu", ctypes.c_double),
         ("max_iter", ctypes.c_int32),
+    ]
+
+
+_B, _S = OSC_KIN_MAX_BODIES, OSC_KIN_MAX_SITES
+
+
+class OscKinDesc(ctypes.Structure):
+    """osc_kin_desc (include/osc_kinematics.h): mjModel's body / joint / site fields."""
+    _fields_ = [
+        ("nbody", ctypes.c_int32), ("nsite", ctypes.c_int32),
+        ("gravity", ctypes.c_double * 3),
+        ("parent", ctypes.c_int32 * _B), ("jnt_type", ctypes.c_int32 * _B),
+        ("pos", (ctypes.c_double * 3) * _B), ("quat", (ctypes.c_double * 4) * _B),
+        ("axis", (ctypes.c_double * 3) * _B), ("jnt_pos", (ctypes.c_double * 3) * _B),
+        ("armature", ctypes.c_double * _B), ("mass", ctypes.c_double * _B),
+        ("ipos", (ctypes.c_double * 3) * _B), ("iquat", (ctypes.c_double * 4) * _B),
+        ("inertia", (ctypes.c_double * 3) * _B),
+        ("site_body", ctypes.c_int32 * _S), ("site_pos", (ctypes.c_double * 3) * _S),
     ]
 
 
@@ -87,6 +114,27 @@ def lib() -> ctypes.CDLL:
     L.osc_pd_base_targets.restype = ctypes.c_int
     L.osc_contact_mask_from_contacts.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, vp]
     L.osc_contact_mask_from_contacts.restype = ctypes.c_int
+    kp = ctypes.POINTER(OscKinDesc)
+    L.osc_kin_desc_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, kp]
+    L.osc_kin_desc_from_json.restype = ctypes.c_int
+    L.osc_kin_model_create.argtypes = [kp, ctypes.POINTER(vp)]
+    L.osc_kin_model_create.restype = ctypes.c_int
+    L.osc_kin_model_create_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p,
+                                                 ctypes.POINTER(vp)]
+    L.osc_kin_model_create_from_json.restype = ctypes.c_int
+    L.osc_kin_model_destroy.argtypes = [vp]
+    L.osc_kin_model_destroy.restype = ctypes.c_int
+    ip = ctypes.POINTER(ctypes.c_int32)
+    L.osc_kin_model_dims.argtypes = [vp, ip, ip, ip]
+    L.osc_kin_model_dims.restype = ctypes.c_int
+    L.osc_batch_kinematics.argtypes = [vp, i32] + [vp] * 7 + [vp]
+    L.osc_batch_kinematics.restype = ctypes.c_int
+    L.osc_state_to_qpos.argtypes = [i32, i32] + [vp] * 7 + [vp]
+    L.osc_state_to_qpos.restype = ctypes.c_int
+    L.osc_qpos_workspace_bytes.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_size_t)]
+    L.osc_qpos_workspace_bytes.restype = ctypes.c_int
+    L.osc_batch_solve_qpos.argtypes = [vp, vp, i32] + [vp] * 9 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_qpos.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -97,4 +145,38 @@ def desc_from_yaml(robot: str, yaml_path: str | None = None) -> OscModelDesc:
                                   ctypes.byref(d))
     if rc != 0:
         raise OSCError("osc_desc_from_yaml", rc)
+    return d
+
+
+def kin_desc_from_json(robot: str, json_path: str | None = None) -> OscKinDesc:
+    d = OscKinDesc()
+    rc = lib().osc_kin_desc_from_json(robot.encode() if robot else None,
+                                      json_path.encode() if json_path else None, ctypes.byref(d))
+    if rc != 0:
+        raise OSCError("osc_kin_desc_from_json", rc)
+    return d
+
+
+def kin_desc_from_dict(tree: dict) -> OscKinDesc:
+    """osc_kin_desc from the <robot>_kinematics.json schema already parsed into a dict."""
+    d = OscKinDesc()
+    bodies, sites = tree["bodies"], tree["sites"]
+    d.nbody, d.nsite = len(bodies), len(sites)
+    d.gravity[:] = tree["gravity"]
+    jt = {"free": JOINT_FREE, "hinge": JOINT_HINGE, "none": JOINT_NONE}
+    for i, b in enumerate(bodies):
+        d.parent[i] = b["parent"]
+        d.jnt_type[i] = jt[b["joint"]]
+        d.pos[i][:] = b["pos"]
+        d.quat[i][:] = b["quat"]
+        d.axis[i][:] = b.get("axis", [0.0, 0.0, 1.0])
+        d.jnt_pos[i][:] = b.get("jnt_pos", [0.0, 0.0, 0.0])
+        d.armature[i] = b.get("armature", 0.0)
+        d.mass[i] = b["mass"]
+        d.ipos[i][:] = b["ipos"]
+        d.iquat[i][:] = b["iquat"]
+        d.inertia[i][:] = b["diaginertia"]
+    for k, s in enumerate(sites):
+        d.site_body[k] = s["body"]
+        d.site_pos[k][:] = s["pos"]
     return d

@@ -20,12 +20,12 @@ OUT_CTRL = os.path.join(PKG_DIR, "lib", "libosc_controller.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_producers.hip"]
+SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_producers.hip", "osc_kinematics.hip"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    hdrs = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h")]
+    hdrs = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h", "osc_kinematics.h")]
     if not force and os.path.exists(OUT):
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):

@@ -68,9 +68,9 @@ class KinModel:
                 nv += 1
         self.nq, self.nv, self.ns = nq, nv, len(self.sites)
         self.armature = np.zeros(nv)
-        for b, da in zip(self.bodies, self.dadr):
-            if b["joint"] == "hinge":
-                self.armature[da] = b["armature"]
+        for b, da in zip(self.bodies, self.dadr):   # dof_armature: every dof of the joint
+            ndof = {"free": 6, "hinge": 1}.get(b["joint"], 0)
+            self.armature[da:da + ndof] = b.get("armature", 0.0)
         # body inertia about the COM, body frame
         self.Ibody = [quat2mat(b["iquat"]) @ np.diag(b["diaginertia"]) @ quat2mat(b["iquat"]).T
                       for b in self.bodies]

@@ -1,0 +1,44 @@
+"""Random kinematic trees (test data) in the <robot>_kinematics.json schema.
+
+The illustrative Go2 / WaLTER trees have identity body quaternions, zero joint anchors and
+diagonal inertias; these exercise every term the kernel and the oracle carry: rotated body
+frames, hinge anchors off the body origin, rotated principal axes, welded bodies, non-unit
+axes, armature, a fixed-base (hinge-rooted) variant and deeper chains."""
+import numpy as np
+
+
+def _unit_quat(rng):
+    q = rng.standard_normal(4)
+    return list(q / np.linalg.norm(q))
+
+
+def random_tree(seed: int, nbody: int = 11, free_root: bool = True, nsite: int = 9,
+                weld_p: float = 0.15) -> dict:
+    rng = np.random.default_rng(seed)
+    bodies = []
+    for i in range(nbody):
+        if i == 0:
+            parent, joint = -1, ("free" if free_root else "hinge")
+        else:
+            parent = int(rng.integers(0, i))
+            joint = "none" if rng.uniform() < weld_p else "hinge"
+        bodies.append(dict(
+            name=f"b{i}", parent=parent, pos=list(0.2 * rng.standard_normal(3)),
+            quat=_unit_quat(rng), joint=joint,
+            axis=list(rng.standard_normal(3) * rng.uniform(0.5, 2.0)),
+            jnt_pos=list(0.05 * rng.standard_normal(3)),
+            armature=float(rng.uniform(0.0, 0.05)) if joint != "free" else 0.0,
+            mass=float(rng.uniform(0.2, 3.0)), ipos=list(0.05 * rng.standard_normal(3)),
+            iquat=_unit_quat(rng), diaginertia=list(rng.uniform(1e-3, 2e-2, size=3))))
+    sites = [dict(name=f"s{k}", body=int(rng.integers(0, nbody)),
+                  pos=list(0.1 * rng.standard_normal(3))) for k in range(nsite)]
+    return dict(name=f"random tree {seed}", gravity=[0.0, 0.0, -9.81], bodies=bodies,
+                sites=sites)
+
+
+def chain_tree(seed: int, nbody: int = 16) -> dict:
+    """A single 15-hinge chain under a free root: the deepest tree the kernel allows."""
+    t = random_tree(seed, nbody=nbody, nsite=12, weld_p=0.0)
+    for i, b in enumerate(t["bodies"][1:], start=1):
+        b["parent"] = i - 1
+    return t

@@ -12,7 +12,7 @@ from osc_amd import _lib
 from osc_qp import load_model
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h", "osc_kinematics.h")]
 REF_CONFIG = "/root/reference/config"
 
 
@@ -87,3 +87,35 @@ def test_no_device_is_reported_not_faked():
     h = ctypes.c_void_p()
     d = _lib.desc_from_yaml("unitree_go2")
     assert _lib.lib().osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 5
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
+def test_kin_desc_from_json_matches_python_reader(robot):
+    """The library's JSON reader and the Python one fill identical descriptors."""
+    import ctypes as ct
+    from osc_amd.kinematics import kin_json_path, load_tree
+    a = _lib.kin_desc_from_json(None, kin_json_path(robot))
+    b = _lib.kin_desc_from_dict(load_tree(robot))
+    assert ct.string_at(ct.addressof(a), ct.sizeof(a)) == ct.string_at(ct.addressof(b), ct.sizeof(b))
+    assert _lib.kin_desc_from_json(robot).nbody == a.nbody    # default path next to the library
+
+
+def test_kin_desc_errors():
+    with pytest.raises(_lib.OSCError) as e:
+        _lib.kin_desc_from_json(None, "/nonexistent/tree.json")
+    assert e.value.code == 3
+    import ctypes as ct
+    from kin_trees import random_tree
+    L = _lib.lib()
+    bad = [lambda d: setattr(d, "nbody", 17),
+           lambda d: d.parent.__setitem__(3, 5),            # parent after child
+           lambda d: d.jnt_type.__setitem__(2, 0),          # free joint below the root
+           lambda d: d.jnt_type.__setitem__(2, 2),          # slide: not supported
+           lambda d: d.site_body.__setitem__(0, 40),
+           lambda d: [d.axis[1].__setitem__(i, 0.0) for i in range(3)]]
+    for mutate in bad:
+        d = _lib.kin_desc_from_dict(random_tree(1, weld_p=0.0))
+        mutate(d)
+        h = ct.c_void_p()
+        assert L.osc_kin_model_create(ct.byref(d), ct.byref(h)) == 1
+    assert L.osc_batch_kinematics(None, 1, *([None] * 7), None) == 1

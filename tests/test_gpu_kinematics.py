@@ -1,0 +1,138 @@
+"""GPU parity of the kinematics front end (osc_batch_kinematics, osc_state_to_qpos,
+osc_batch_solve_qpos; include/osc_kinematics.h) against the CPU kinematics oracle
+(oracle/kinematics.py: COM-Jacobian / Kane formulation, pinned by finite-difference and energy
+identities in test_kinematics_oracle.py; parity against MuJoCo itself is unpinned -- no MuJoCo,
+no robot XMLs offline).
+
+Tolerance (fp64, two different formulations of the same quantities): per environment and per
+output, max |gpu - oracle| <= 1e-12 * (1 + max |oracle|).  M must be exactly symmetric."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import kinematics as kin
+from kin_trees import chain_tree, random_tree
+from osc_amd.kinematics import KinematicsBatch, load_tree, random_states
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-12
+
+
+def _trees():
+    return {"unitree_go2": load_tree("unitree_go2"), "walter_sr": load_tree("walter_sr"),
+            "random_free": random_tree(5), "random_fixed": random_tree(6, free_root=False),
+            "chain16": chain_tree(7)}
+
+
+TREES = _trees()
+
+
+def _check(tree, nenv, seed, base_pos_zero=True):
+    kb = KinematicsBatch(tree=tree)
+    qpos, qvel = random_states(tree, nenv, seed, base_pos_zero=base_pos_zero)
+    out = kb.compute(qpos, qvel)
+    torch.cuda.synchronize()
+    M, C, J, b, X = (t.cpu().numpy() for t in (out.M, out.C, out.J, out.b, out.site_xpos))
+    m = kin.KinModel(tree)
+    for e in range(nenv):
+        Mr, Cr, Jr, br = kin.kinematics(m, qpos[e], qvel[e])
+        Xr = kin.site_positions(m, qpos[e])
+        for name, got, ref in (("M", M[e], Mr), ("C", C[e], Cr), ("J", J[e], Jr), ("b", b[e], br),
+                               ("site_xpos", X[e], Xr)):
+            err = np.abs(got - ref).max()
+            assert err <= TOL * (1 + np.abs(ref).max()), (name, e, err)
+        assert np.array_equal(M[e], M[e].T)
+    return kb
+
+
+@pytest.mark.parametrize("name", list(TREES))
+def test_kinematics_matches_oracle(gpu, name):
+    # 37 envs: 9 full wavefronts + a ragged tail row
+    _check(TREES[name], 37, 100 + len(name), base_pos_zero=(name != "random_free"))
+
+
+def test_single_env_and_empty_batch(gpu):
+    kb = _check(TREES["unitree_go2"], 1, 3)
+    out = kb.alloc(0)
+    empty = torch.empty((0, kb.nq), dtype=torch.float64, device=gpu)
+    kb.compute_into(out, empty, torch.empty((0, kb.nv), dtype=torch.float64, device=gpu))
+
+
+def test_large_batch_properties(gpu):
+    """65,536 Go2 envs: M symmetric positive definite, J structure = the tree's (feet rows touch
+    base + own leg only), gravity-only bias at zero velocity equals the total weight on base z,
+    and a sample of environments matches the oracle."""
+    tree = TREES["unitree_go2"]
+    kb = KinematicsBatch(tree=tree)
+    nenv = 65536
+    qpos, qvel = random_states(tree, nenv, 77)
+    out = kb.compute(qpos, qvel, want_sites=False)
+    M = out.M
+    assert torch.equal(M, M.transpose(1, 2))
+    assert torch.linalg.eigvalsh(M).min().item() > 0
+    J = out.J.cpu().numpy()
+    m = kin.KinModel(tree)
+    for k, s in enumerate(m.sites):
+        chain = set()
+        for c in m.chain(s["body"]):
+            nd = {"free": 6, "hinge": 1}.get(m.bodies[c]["joint"], 0)
+            chain |= set(range(m.dadr[c], m.dadr[c] + nd))
+        off = [d for d in range(m.nv) if d not in chain]
+        assert np.all(J[:, 3 * k:3 * k + 3, off] == 0.0)
+        assert np.all(J[:, 3 * m.ns + 3 * k:3 * m.ns + 3 * k + 3, off] == 0.0)
+    g = kb.compute(qpos[:64], np.zeros((64, kb.nv))).C.cpu().numpy()
+    total = sum(b["mass"] for b in tree["bodies"])
+    np.testing.assert_allclose(g[:, 2], total * 9.81, rtol=1e-13)
+    for e in (0, 12345, nenv - 1):
+        Mr, Cr, Jr, br = kin.kinematics(m, qpos[e], qvel[e])
+        assert np.abs(M[e].cpu().numpy() - Mr).max() <= TOL * (1 + np.abs(Mr).max())
+        assert np.abs(out.b[e].cpu().numpy() - br).max() <= TOL * (1 + np.abs(br).max())
+
+
+def test_state_to_qpos_packing(gpu):
+    """update_mj_data (osc.h:357-361): qpos = [0,0,0, quat, q_m], qvel = [v, w, qd_m]."""
+    kb = KinematicsBatch("unitree_go2")
+    rng = np.random.default_rng(4)
+    n, nu = 33, 12
+    rot = rng.standard_normal((n, 4))
+    lin, ang = rng.standard_normal((n, 3)), rng.standard_normal((n, 3))
+    qm, qdm = rng.standard_normal((n, nu)), rng.standard_normal((n, nu))
+    qpos, qvel = kb.state_to_qpos(rot, lin, ang, qm, qdm)
+    np.testing.assert_array_equal(qpos.cpu().numpy(), np.hstack([np.zeros((n, 3)), rot, qm]))
+    np.testing.assert_array_equal(qvel.cpu().numpy(), np.hstack([lin, ang, qdm]))
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
+def test_solve_from_joint_states(gpu, robot):
+    """osc_batch_solve_qpos == osc_batch_kinematics + osc_batch_solve (bitwise), and its torques
+    match the oracle chain (oracle kinematics -> reference QP -> exact optimum) within the solve's
+    parity tolerance (test_gpu_parity.py)."""
+    from osc_amd.solver import OSCBatchSolver
+    from osc_amd.synth import SEED_BASE
+    from osc_qp import build_qp, load_model, torque
+    from qp_exact import solve_exact
+    tree = load_tree(robot)
+    kb = KinematicsBatch(tree=tree)
+    solver = OSCBatchSolver(robot)
+    nenv = 24
+    qpos, qvel = random_states(tree, nenv, SEED_BASE + 9, joint_range=0.5)
+    rng = np.random.default_rng(9)
+    ns, nc = solver.dims["ns"], solver.dims["nc"]
+    T = np.zeros((nenv, ns, 6))
+    T[:, 0, :] = 10.0 * rng.standard_normal((nenv, 6))
+    mask = (rng.uniform(size=(nenv, nc)) < 0.75).astype(np.float64)
+    res = kb.solve(solver, qpos, qvel, T, mask, want_x=True)
+    k = kb.compute(qpos, qvel, want_sites=False)
+    ref = solver.solve(k.M, k.C, k.J, k.b, T, mask, want_x=True)
+    torch.cuda.synchronize()
+    assert torch.equal(res.tau, ref.tau) and torch.equal(res.x, ref.x)
+    assert (res.status.cpu().numpy() == 0).all(), res.status
+    model = load_model(robot)
+    m = kin.KinModel(tree)
+    tau = res.tau.cpu().numpy()
+    for e in range(nenv):
+        M, C, J, b = kin.kinematics(m, qpos[e], qvel[e])
+        args = (M, C, J, b, T[e], mask[e])
+        tr = torque(model, solve_exact(model, build_qp(model, *args), M, C, J).x)
+        assert np.abs(tau[e] - tr).max() / max(np.abs(tr).max(), 1.0) <= 1e-5, e

@@ -15,9 +15,20 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "oracle"))
 import kinematics as kin  # noqa: E402
+from kin_trees import chain_tree, random_tree  # noqa: E402
 
-ROBOTS = ["unitree_go2", "walter_sr"]
+ROBOTS = ["unitree_go2", "walter_sr", "random_free", "random_fixed", "chain"]
 EPS = 1e-6
+
+
+def _load(name):
+    if name == "random_free":
+        return kin.KinModel(random_tree(5))
+    if name == "random_fixed":
+        return kin.KinModel(random_tree(6, free_root=False))
+    if name == "chain":
+        return kin.KinModel(chain_tree(7))
+    return kin.load(name)
 
 
 def _rot_vee(Rd):
@@ -26,7 +37,7 @@ def _rot_vee(Rd):
     return np.array([A[2, 1], A[0, 2], A[1, 0]])
 
 
-@pytest.mark.parametrize("robot", ROBOTS)
+@pytest.mark.parametrize("robot", ROBOTS[:2])
 def test_sizes_match_the_qp_models(robot):
     m = kin.load(robot)
     nv, ns = {"unitree_go2": (18, 5), "walter_sr": (14, 17)}[robot]
@@ -35,7 +46,7 @@ def test_sizes_match_the_qp_models(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_jacobians_match_finite_differences(robot):
-    m = kin.load(robot)
+    m = _load(robot)
     rng = np.random.default_rng(11)
     for _ in range(3):
         q, v = kin.random_state(m, rng, base_pos_zero=False)
@@ -53,7 +64,7 @@ def test_jacobians_match_finite_differences(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_jdot_qdot_matches_finite_differences(robot):
-    m = kin.load(robot)
+    m = _load(robot)
     rng = np.random.default_rng(12)
     for _ in range(3):
         q, v = kin.random_state(m, rng)
@@ -66,7 +77,7 @@ def test_jdot_qdot_matches_finite_differences(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_mass_matrix_is_the_kinetic_energy(robot):
-    m = kin.load(robot)
+    m = _load(robot)
     rng = np.random.default_rng(13)
     for _ in range(3):
         q, v = kin.random_state(m, rng)
@@ -89,7 +100,7 @@ def test_mass_matrix_is_the_kinetic_energy(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_bias_gravity_and_energy_balance(robot):
-    m = kin.load(robot)
+    m = _load(robot)
     rng = np.random.default_rng(14)
     for _ in range(3):
         q, v = kin.random_state(m, rng)
