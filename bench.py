@@ -74,6 +74,50 @@ def cpu_baseline(robot: str, seconds: float, cores: int) -> dict:
                       f"iters/tick); single core alone {rate1:.0f} solves/s"}
 
 
+def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
+    """the GPU kinematics front end (osc_batch_kinematics: qpos/qvel ->
+    M, C, J, b) and the whole tick from joint states (osc_batch_solve_qpos), timed with HIP
+    events on the launch stream.  Not part of `value` (the headline excludes MuJoCo/kinematics
+    on both sides)."""
+    from osc_amd.kinematics import KinematicsBatch, load_tree, random_states
+    tree = load_tree(robot)
+    kb = KinematicsBatch(tree=tree)
+    qpos, qvel = random_states(tree, nenv, seed, joint_range=0.5)
+    qpos = torch.from_numpy(qpos).cuda()
+    qvel = torch.from_numpy(qvel).cuda()
+    kout = kb.alloc(nenv)
+    d = generate(robot, nenv, seed, "standing", "ones")
+    T = torch.from_numpy(d["T"]).cuda()
+    mask = torch.from_numpy(d["mask"]).cuda()
+    out = solver.alloc_outputs(nenv)
+    ws = torch.empty((kb.workspace_bytes(solver, nenv) // 8 + 2,), dtype=torch.float64,
+                     device=qpos.device)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps
+
+    kin_ms = timed(lambda: kb.compute_into(kout, qpos, qvel))
+    tick_ms = timed(lambda: kb.solve_into(solver, out, qpos, qvel, T, mask, ws))
+    nq, nv, ns = kb.nq, kb.nv, kb.ns
+    kin_bytes = 8 * (nq + nv + nv * nv + nv + 6 * ns * nv + 6 * ns)
+    gbs = kin_bytes * nenv / (kin_ms * 1e-3) / 1e9
+    return {"kernel": "osc_kinematics_kernel", "tree": tree["name"], "envs": nenv,
+            "kinematics_ms": kin_ms,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "bytes_per_env": kin_bytes},
+            "tick_from_joint_states_ms": tick_ms,
+            "tick_from_joint_states_solves_per_s": nenv / (tick_ms * 1e-3)}
+
+
 def baseline_config_tag(args, nenv):
     """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
     tags = {("unitree_go2", "standing", "ones", 4096): 1,
@@ -96,6 +140,8 @@ def main() -> None:
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1),
                     help="CPU baseline worker processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-front-end", action="store_true",
+                    help="skip the kinematics front-end timing (reported beside the headline)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -190,6 +236,9 @@ def main() -> None:
                               "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
             "converged_frac": converged,
         }
+        if not args.no_front_end:
+            line["front_end"] = front_end(args.robot, solver, nenv, args.steps, args.warmup,
+                                          shard_seed(rank), stream)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.robot, args.cpu_seconds, args.cpu_cores)
         print(json.dumps(line), flush=True)

@@ -63,7 +63,7 @@ constexpr int B_R = 0, B_X = 9, B_W = 12, B_VO = 15, B_AL = 18, B_AO = 21, B_M =
               B_IO = 28, B_F = 34;   // IO: xx yy zz xy xz yz;  F: (n, f) total force
 
 // Device-resident model tables (derived on the host from osc_kin_desc).
-struct KinDev {
+struct alignas(16) KinDev {   // alignas: sizeof % 16 == 0 (16-byte LDS staging)
   int32_t nbody, nq, nv, nsite, ndepth;
   int32_t parent[OSC_KIN_MAX_BODIES];
   int32_t jtype[OSC_KIN_MAX_BODIES];
@@ -126,7 +126,7 @@ __device__ __forceinline__ void inertia_mul(double m, const double* h, const dou
 
 // Forward pass for body b (its parent's state is final): frame, velocity, bias acceleration,
 // spatial inertia and the body's own RNEA force.  Writes the body's LDS state.
-__device__ void body_forward(const KinDev* __restrict__ K, double* E, const EnvLayout& lay,
+__device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
                              int b) {
   double R[9], x[3], w[3], vo[3], al[3], ao[3];
   const int jt = K->jtype[b];
@@ -265,16 +265,28 @@ __device__ void body_forward(const KinDev* __restrict__ K, double* E, const EnvL
 }
 
 __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
-    const KinDev* __restrict__ K, int nenv, const double* __restrict__ qpos,
+    const KinDev* __restrict__ Kg, int nenv, const double* __restrict__ qpos,
     const double* __restrict__ qvel, double* __restrict__ gM, double* __restrict__ gC,
     double* __restrict__ gJ, double* __restrict__ gb, double* __restrict__ gx) {
   extern __shared__ __attribute__((aligned(16))) double kin_sm[];
+  // The model tables are indexed per lane (body / dof / site differ across lanes), so they are
+  // staged into LDS once per workgroup: ~64-cycle LDS reads instead of dependent L2 round trips
+  // in every output-element iteration.
+  __shared__ __attribute__((aligned(16))) KinDev sK;
+  {
+    static_assert(sizeof(KinDev) % 16 == 0, "16-byte staging of the model tables");
+    const uint4* src = reinterpret_cast<const uint4*>(Kg);
+    uint4* dst = reinterpret_cast<uint4*>(&sK);
+    for (int i = threadIdx.x; i < static_cast<int>(sizeof(KinDev) / 16); i += kWave) dst[i] = src[i];
+  }
+  wave_sync();
+  const KinDev* K = &sK;
   const int lane = threadIdx.x;
   const int row = lane / kRow, l = lane % kRow;
   const int env_raw = blockIdx.x * kEnvPerWave + row;
   const bool valid = env_raw < nenv;
   const int env = valid ? env_raw : nenv - 1;   // tail rows recompute the last env, store nothing
-  const int nq = K->nq, nv = K->nv, nb = K->nbody, ns = K->nsite, nd = K->ndepth;
+  const int nq = Kg->nq, nv = Kg->nv, nb = Kg->nbody, ns = Kg->nsite, nd = Kg->ndepth;
   const EnvLayout lay(nq, nv, nb, ns);
   double* E = kin_sm + row * lay.size;
 
