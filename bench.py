@@ -118,6 +118,68 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
             "tick_from_joint_states_solves_per_s": nenv / (tick_ms * 1e-3)}
 
 
+def run_mixed(args, world, rank, dev, barrier) -> None:
+    """BASELINE configs[4]: mixed Go2 + WaLTER Sr.  Every rank solves its own shard of
+    --nenv-per-gpu Go2 envs AND --nenv-per-gpu WaLTER envs (4,096 + 4,096 per GPU: 65,536 over 8
+    GPUs), the two models launched on two streams so their kernels overlap.  A
+    step = both shards solved; value = all envs of all ranks / max-over-ranks time."""
+    from osc_amd.solver import OSCBatchSolver
+    nenv = args.nenv_per_gpu
+    robots = ("unitree_go2", "walter_sr")
+    main = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in robots]
+    jobs = []
+    for i, robot in enumerate(robots):
+        solver = OSCBatchSolver(robot)
+        d = generate(robot, nenv, shard_seed(rank) + 500 * i, args.scenario, args.mask)
+        jobs.append((solver, solver.prepare(**d), solver.alloc_outputs(nenv)))
+
+    def step():
+        for st, (solver, inputs, out) in zip(streams, jobs):
+            st.wait_stream(main)
+            solver.solve_into(out, *inputs, stream=st)
+        for st in streams:
+            main.wait_stream(st)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(main)
+    for _ in range(args.steps):
+        step()
+    e1.record(main)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    conv = sum(int((o.status == 0).sum().item()) for _, _, o in jobs)
+    stats = reduce_stats(world, dev, 2 * nenv, elapsed, kernel_ms, 0.0, conv)
+    if rank != 0:
+        return
+    value = job_value(stats, args.steps)
+    bps = (bytes_per_solve("unitree_go2") + bytes_per_solve("walter_sr")) * nenv
+    achieved = bps / (stats.kernel_ms * 1e-3) / 1e9
+    print(json.dumps({
+        "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": stats.elapsed_s / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded post-kinematics M, C, J, b, T, mask; osc_amd.synth)",
+        "config": {"workload": f"mixed unitree_go2 + walter_sr {args.scenario} mask={args.mask}, "
+                               f"{nenv} + {nenv} envs per GPU (BASELINE configs[4] at 8 GPUs)",
+                   "robot": "mixed", "envs_per_gpu": 2 * nenv, "global_envs": stats.total_envs,
+                   "parallelism": f"env-shard x{world}, 2 streams per GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "osc_setup_kernel + osc_ipm_kernel x 2 models, 2 streams",
+                     "kernel_ms": stats.kernel_ms},
+        "converged_frac": stats.converged}), flush=True)
+
+
 def baseline_config_tag(args, nenv):
     """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
     tags = {("unitree_go2", "standing", "ones", 4096): 1,
@@ -142,6 +204,9 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-front-end", action="store_true",
                     help="skip the kinematics front-end timing (reported beside the headline)")
+    ap.add_argument("--mask-redraw", type=int, default=0,
+                    help="cycle through this many Bernoulli masks, one per step (configs[3]: "
+                         "contact-mode switching, walter_sr_true_tumbling_mjjoint.cc:554-614)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -156,6 +221,12 @@ def main() -> None:
     def barrier():
         dist_barrier(world)
 
+    if args.robot == "mixed":
+        run_mixed(args, world, rank, dev, barrier)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
     from osc_amd.solver import OSCBatchSolver
     nenv = args.nenv_per_gpu
     solver = OSCBatchSolver(args.robot)
@@ -163,6 +234,13 @@ def main() -> None:
     inputs = solver.prepare(**d)
     out = solver.alloc_outputs(nenv)
     stream = torch.cuda.current_stream(dev)
+    # per-step contact masks (mask switching): step k assembles and solves with masks[k % K]
+    masks = [inputs[5]]
+    if args.mask_redraw > 0:
+        rng = np.random.default_rng(shard_seed(rank) + 1)
+        nc = inputs[5].shape[1]
+        masks = [torch.from_numpy((rng.uniform(size=(nenv, nc)) < 0.75).astype(np.float64))
+                 .to(dev) for _ in range(args.mask_redraw)]
 
     for _ in range(args.warmup):
         solver.solve_into(out, *inputs)
@@ -172,13 +250,13 @@ def main() -> None:
     # kernel), the two halves of osc_batch_solve, with HIP events on the launch stream around
     # each kernel.
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    mask = inputs[5]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
+        mask = masks[k % len(masks)]
         ev[k][0].record(stream)
-        solver.assemble_into(out, *inputs)
+        solver.assemble_into(out, *inputs[:5], mask)
         ev[k][1].record(stream)
         solver.solve_assembled_into(out, mask)
         ev[k][2].record(stream)
@@ -221,7 +299,8 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded post-kinematics M, C, J, b, T, mask; osc_amd.synth)",
-            "config": {"workload": f"{args.robot} {args.scenario} mask={args.mask}, "
+            "config": {"workload": f"{args.robot} {args.scenario} mask={args.mask}"
+                                   f"{f' redrawn per step ({args.mask_redraw} masks)' if args.mask_redraw else ''}, "
                                    f"{nenv} envs per GPU{baseline_config_tag(args, nenv)}",
                        "robot": args.robot, "envs_per_gpu": nenv, "global_envs": total,
                        "parallelism": f"env-shard x{world}"},

@@ -6,20 +6,26 @@
  * unitree_go2/operational_space_controller.h:106-238, 546-589 (walter_sr/... identical), with
  * three deliberate differences, each forced by what this build can and cannot link:
  *
- *  1. Kinematics is injected.  The reference owns an mjModel/mjData and runs update_mj_data +
- *     update_osc_data (operational_space_controller.h:350-455) each tick.  MuJoCo and the robot
- *     XMLs are not part of this library; the caller passes a KinematicsFn computing exactly
- *     what update_osc_data stores in OSCData (M = mj_fullM, C = qfrc_bias, J = [Jp; Jr],
- *     b = [Jpd; Jrd] qvel) from the State.  A maintainer wires it to their mjData in ~20 lines
- *     (INTEGRATION.md §5).
+ *  1. Kinematics.  The reference owns an mjModel/mjData and runs update_mj_data +
+ *     update_osc_data (operational_space_controller.h:350-455) each tick.  MuJoCo is not part
+ *     of this library, so the controller either
+ *       (a) runs the GPU kinematics front end (include/osc_kinematics.h) on the robot's
+ *           kinematic tree (<robot>_kinematics.json or any osc_kin_desc-schema JSON): the State
+ *           is packed exactly as update_mj_data packs qpos/qvel (:357-361) and the whole tick is
+ *           osc_batch_solve_qpos -- the constructor without a KinematicsFn; or
+ *       (b) takes a caller's KinematicsFn computing what update_osc_data stores in OSCData
+ *           (M = mj_fullM, C = qfrc_bias, J = [Jp; Jr], b = [Jpd; Jrd] qvel), e.g. from the
+ *           caller's own mjData.
  *  2. Sizes are runtime values from the YAML config (osc_desc_from_yaml) instead of the
  *     autogen_defines.h constants, so one class serves Go2 and WaLTER.  Vectors are
  *     std::vector<double>, matrices row-major (the reference's Eigen layout, aliases.h:12-13).
  *  3. Status stands in for absl::Status (same codes the reference uses: OK,
  *     FailedPrecondition, Internal, InvalidArgument).
  *
- * Per tick (the reference's control_loop body, :556-574): under the mutex, kinematics(state) ->
- * host->device copies -> osc_batch_solve(nenv = 1) -> torque_command = x[nv : nv+nu].
+ * Per tick (the reference's control_loop body, :556-574), under the mutex:
+ *   (a) pack qpos/qvel -> one host->device copy -> osc_batch_solve_qpos(nenv = 1), or
+ *   (b) kinematics(state) -> host->device copy -> osc_batch_solve(nenv = 1),
+ * then torque_command = x[nv : nv+nu].
  * step() runs one such tick synchronously (for callers without the thread, and tests).
  */
 #ifndef OSC_CONTROLLER_H_
@@ -33,6 +39,7 @@
 #include <vector>
 
 #include "osc_batch.h"
+#include "osc_kinematics.h"
 
 namespace osc_amd {
 
@@ -85,6 +92,10 @@ class OperationalSpaceController {
    * (empty = the robot's default config); control_rate_us as the reference (default 2000). */
   OperationalSpaceController(std::string robot, std::string yaml_path, KinematicsFn kinematics,
                              int control_rate_us = 2000);
+  /* GPU kinematics front end: kin_json_path = the kinematic tree (empty = the robot's default
+   * <robot>_kinematics.json next to the library's config directory). */
+  explicit OperationalSpaceController(std::string robot, std::string yaml_path = "",
+                                      int control_rate_us = 2000, std::string kin_json_path = "");
   ~OperationalSpaceController();
   OperationalSpaceController(const OperationalSpaceController&) = delete;
   OperationalSpaceController& operator=(const OperationalSpaceController&) = delete;
@@ -116,8 +127,14 @@ class OperationalSpaceController {
   void control_loop();
   void release_device();
 
-  std::string robot_, yaml_path_;
+  Status tick_gpu_kinematics_locked();
+  Status fetch_outputs_locked();
+
+  std::string robot_, yaml_path_, kin_json_path_;
   KinematicsFn kinematics_;
+  bool gpu_kinematics_ = false;
+  osc_kin_model* kin_ = nullptr;
+  int nq_ = 0;
   int control_rate_us_;
   osc_model_desc desc_{};
   int nv_ = 0, nu_ = 0, nc_ = 0, ns_ = 0, n_ = 0;
@@ -134,7 +151,8 @@ class OperationalSpaceController {
 
   osc_model* model_ = nullptr;
   void* stream_ = nullptr;
-  double* d_in_ = nullptr;          // M | C | J | b | T | mask (one allocation, 16-B aligned)
+  double* d_in_ = nullptr;          // M | C | J | b | T | mask, or qpos | qvel | T | mask
+                                    // (one allocation, blocks 16-B aligned)
   double* d_out_ = nullptr;         // tau | x
   int32_t* d_info_ = nullptr;       // status | iters
   void* d_ws_ = nullptr;

@@ -36,6 +36,16 @@ OperationalSpaceController::OperationalSpaceController(std::string robot, std::s
       kinematics_(std::move(kinematics)),
       control_rate_us_(control_rate_us) {}
 
+OperationalSpaceController::OperationalSpaceController(std::string robot, std::string yaml_path,
+                                                       int control_rate_us,
+                                                       std::string kin_json_path)
+    : robot_(std::move(robot)),
+      yaml_path_(std::move(yaml_path)),
+      kin_json_path_(std::move(kin_json_path)),
+      control_rate_us_(control_rate_us) {
+  gpu_kinematics_ = true;
+}
+
 OperationalSpaceController::~OperationalSpaceController() {
   if (thread_initialized_ && thread_.joinable()) {
     running_ = false;
@@ -57,7 +67,13 @@ Status OperationalSpaceController::initialize(State initial_state) {
   n_ = nv_ + nu_ + 3 * nc_;
   if (initial_state.contact_mask.size() != static_cast<size_t>(nc_))
     return InvalidArgumentError("State.contact_mask must have one entry per contact site");
-  if (!kinematics_) return InvalidArgumentError("no kinematics provider");
+  if (!kinematics_ && !gpu_kinematics_) return InvalidArgumentError("no kinematics provider");
+  if (gpu_kinematics_ &&
+      (initial_state.motor_position.size() != static_cast<size_t>(nu_) ||
+       initial_state.motor_velocity.size() != static_cast<size_t>(nu_) ||
+       initial_state.body_rotation.size() != 4 || initial_state.linear_body_velocity.size() != 3 ||
+       initial_state.angular_body_velocity.size() != 3))
+    return InvalidArgumentError("State sizes do not match the robot (nu motors, 4 + 3 + 3 base)");
   std::lock_guard<std::mutex> lock(mutex_);
   state_ = std::move(initial_state);
   targets_.assign(static_cast<size_t>(ns_) * 6, 0.0);   // TaskspaceTargets::Zero()  (:243)
@@ -73,9 +89,33 @@ Status OperationalSpaceController::initialize_optimization() {
   Status st = from_osc(osc_model_create(&desc_, &model_), "osc_model_create");
   if (!st.ok()) return st;
   const size_t s = 6 * static_cast<size_t>(ns_);
-  const size_t in_doubles = even(nv_ * nv_) + even(nv_) + even(s * nv_) + even(s) +
-                            even(ns_ * 6) + even(nc_);
-  if (osc_workspace_bytes(model_, 1, &ws_bytes_) != OSC_OK) return InternalError("workspace size");
+  size_t in_doubles = even(nv_ * nv_) + even(nv_) + even(s * nv_) + even(s) +
+                      even(ns_ * 6) + even(nc_);
+  if (gpu_kinematics_) {
+    // the wheel-weight config drives the same robot as walter_sr
+    const std::string tree = robot_ == "walter_sr_wheels" ? "walter_sr" : robot_;
+    st = from_osc(osc_kin_model_create_from_json(
+                      tree.c_str(), kin_json_path_.empty() ? nullptr : kin_json_path_.c_str(), &kin_),
+                  "osc_kin_model_create_from_json");
+    if (!st.ok()) {
+      release_device();
+      return st;
+    }
+    int32_t nq = 0, nv = 0, nsite = 0;
+    osc_kin_model_dims(kin_, &nq, &nv, &nsite);
+    if (nv != nv_ || nsite != ns_ || nq != 7 + nu_) {   // floating base + one dof per motor
+      release_device();
+      return InvalidArgumentError("kinematic tree does not match the OSC model");
+    }
+    nq_ = nq;
+    in_doubles = even(nq_) + even(nv_) + even(ns_ * 6) + even(nc_);
+    if (osc_qpos_workspace_bytes(model_, kin_, 1, &ws_bytes_) != OSC_OK) {
+      release_device();
+      return InternalError("workspace size");
+    }
+  } else if (osc_workspace_bytes(model_, 1, &ws_bytes_) != OSC_OK) {
+    return InternalError("workspace size");
+  }
   hipStream_t stream = nullptr;
   if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&d_in_), in_doubles * sizeof(double)) != hipSuccess ||
@@ -158,9 +198,48 @@ Status OperationalSpaceController::step() {
   return tick_locked();
 }
 
+// (a) GPU kinematics: update_mj_data's packing (:357-361) on the host, then one copy and the
+// whole tick on the device (osc_batch_solve_qpos).  Caller holds the mutex.
+Status OperationalSpaceController::tick_gpu_kinematics_locked() {
+  if (targets_.size() != static_cast<size_t>(ns_) * 6 ||
+      state_.contact_mask.size() != static_cast<size_t>(nc_) ||
+      state_.motor_position.size() != static_cast<size_t>(nu_) ||
+      state_.motor_velocity.size() != static_cast<size_t>(nu_) || state_.body_rotation.size() != 4 ||
+      state_.linear_body_velocity.size() != 3 || state_.angular_body_velocity.size() != 3)
+    return InvalidArgumentError("State / targets size mismatch");
+  double* h = h_in_.data();
+  double* qpos = h;
+  double* qvel = h + even(nq_);
+  double* T = qvel + even(nv_);
+  double* mask = T + even(ns_ * 6);
+  qpos[0] = qpos[1] = qpos[2] = 0.0;                     // base position forced to 0 (:358-359)
+  std::memcpy(qpos + 3, state_.body_rotation.data(), 4 * sizeof(double));
+  std::memcpy(qpos + 7, state_.motor_position.data(), nu_ * sizeof(double));
+  std::memcpy(qvel, state_.linear_body_velocity.data(), 3 * sizeof(double));
+  std::memcpy(qvel + 3, state_.angular_body_velocity.data(), 3 * sizeof(double));
+  std::memcpy(qvel + 6, state_.motor_velocity.data(), nu_ * sizeof(double));
+  std::memcpy(T, targets_.data(), targets_.size() * sizeof(double));
+  std::memcpy(mask, state_.contact_mask.data(), nc_ * sizeof(double));
+  const size_t off = static_cast<size_t>(mask - h) + even(nc_);
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (hipMemcpyAsync(d_in_, h, off * sizeof(double), hipMemcpyHostToDevice, stream) != hipSuccess)
+    return InternalError("host to device copy failed");
+  return from_osc(osc_batch_solve_qpos(model_, kin_, 1, d_in_, d_in_ + (qvel - h),
+                                       d_in_ + (T - h), d_in_ + (mask - h), d_out_,
+                                       d_out_ + even(nu_), d_info_, d_info_ + 1, d_ws_, ws_bytes_,
+                                       stream_),
+                  "osc_batch_solve_qpos");
+}
+
 // The body of the reference's control_loop (:556-574), caller holds the mutex.
 Status OperationalSpaceController::tick_locked() {
-  Status st = kinematics_(state_, &osc_data_);          // update_mj_data + update_osc_data
+  Status st;
+  if (gpu_kinematics_) {
+    st = tick_gpu_kinematics_locked();
+    if (!st.ok()) return st;
+    return fetch_outputs_locked();
+  }
+  st = kinematics_(state_, &osc_data_);                  // update_mj_data + update_osc_data
   if (!st.ok()) return st;
   const size_t nv = nv_, s = 6 * static_cast<size_t>(ns_);
   if (osc_data_.mass_matrix.size() != nv * nv || osc_data_.coriolis_matrix.size() != nv ||
@@ -191,6 +270,12 @@ Status OperationalSpaceController::tick_locked() {
                                 d_tau, d_x, d_info_, d_info_ + 1, d_ws_, ws_bytes_, stream_),
                 "osc_batch_solve");
   if (!st.ok()) return st;
+  return fetch_outputs_locked();
+}
+
+// Copy tau | x | status | iters back and publish them (torque_command = x[nv : nv+nu], :573).
+Status OperationalSpaceController::fetch_outputs_locked() {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
   std::vector<double> out(even(nu_) + n_);
   int32_t info[2] = {0, 0};
   if (hipMemcpyAsync(out.data(), d_out_, out.size() * sizeof(double), hipMemcpyDeviceToHost,
@@ -235,6 +320,8 @@ void OperationalSpaceController::release_device() {
   if (d_ws_) (void)hipFree(d_ws_);
   if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
   if (model_) (void)osc_model_destroy(model_);
+  if (kin_) (void)osc_kin_model_destroy(kin_);
+  kin_ = nullptr;
   d_in_ = d_out_ = nullptr;
   d_info_ = nullptr;
   d_ws_ = nullptr;

@@ -25,7 +25,8 @@ OK, INVALID_ARGUMENT, FAILED_PRECONDITION, INTERNAL = 0, 3, 9, 13
 
 def driver():
     osc_build.build()
-    deps = [SRC, osc_build.OUT_CTRL, os.path.join(REPO, "include", "osc_controller.h")]
+    deps = [SRC, osc_build.OUT_CTRL, os.path.join(REPO, "include", "osc_controller.h"),
+            os.path.join(REPO, "include", "osc_kinematics.h")]
     if not os.path.exists(EXE) or any(os.path.getmtime(p) > os.path.getmtime(EXE) for p in deps):
         os.makedirs(os.path.dirname(EXE), exist_ok=True)
         subprocess.run([osc_build.HIPCC, "-std=c++17", "-O2", "-I", os.path.join(REPO, "include"),
@@ -75,3 +76,42 @@ def test_controller_tick_and_thread_match_oracle(gpu, case, tmp_path):
     assert out["n"] == dims(robot)["n"]
     assert out["thread"] == OK and out["stop"] == OK and out["clean"] == OK
     assert out["ticks_60ms"] >= 10, out                   # 2000 us control rate
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
+def test_gpu_kinematics_controller_arguments(robot):
+    import torch
+    out = run("gpu_lifecycle", robot)
+    assert out["bad_state"] == INVALID_ARGUMENT           # State sized for another robot
+    assert out["init"] == OK and out["init_nt"] == OK
+    # a missing kinematic tree is a load failure (InternalError, as the XML load at osc.h:117);
+    # without a device the model creation fails first, also InternalError
+    assert out["opt_nt"] == INTERNAL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])
+def test_gpu_kinematics_controller_matches_oracle(gpu, robot, tmp_path):
+    """The controller without a KinematicsFn: State -> qpos/qvel (update_mj_data) -> GPU
+    kinematics -> QP -> torque, against the oracle chain (kinematics oracle -> reference QP ->
+    exact optimum)."""
+    import kinematics as kin
+    from osc_amd.kinematics import load_tree, random_states
+    from osc_qp import build_qp, load_model, torque
+    from qp_exact import solve_exact
+    tree = load_tree(robot)
+    qpos, qvel = random_states(tree, 1, 31, joint_range=0.5)
+    model = load_model(robot)
+    rng = np.random.default_rng(31)
+    T = np.zeros((model.ns, 6))
+    T[0] = 10.0 * rng.standard_normal(6)
+    mask = np.ones(model.nc)
+    mask[1] = 0.0
+    M, C, J, b = kin.kinematics(kin.KinModel(tree), qpos[0], qvel[0])
+    tau = torque(model, solve_exact(model, build_qp(model, M, C, J, b, T, mask), M, C, J).x)
+    fx = tmp_path / "fixture.bin"
+    np.concatenate([qpos[0], qvel[0], T.ravel(), mask, tau]).astype(np.float64).tofile(fx)
+    out = run("qpos", robot, str(fx))
+    assert out["status"] == 0
+    assert out["err_step"] <= 1e-5 and out["err_thread"] <= 1e-5, out
+    assert out["thread"] == OK and out["stop"] == OK and out["clean"] == OK
