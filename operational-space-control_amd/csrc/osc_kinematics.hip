@@ -75,6 +75,9 @@ struct alignas(16) KinDev {   // alignas: sizeof % 16 == 0 (16-byte LDS staging)
   uint32_t anc[OSC_KIN_MAX_BODIES];          // ancestor-or-self body mask
   int32_t dof_body[OSC_KIN_MAX_DOFS];
   int32_t site_body[OSC_KIN_MAX_SITES];
+  uint32_t dof_relmask[OSC_KIN_MAX_DOFS];    // dofs j with M_ij structurally non-zero
+  double dof_arm[OSC_KIN_MAX_DOFS];          // dof_armature
+  uint32_t site_dofmask[OSC_KIN_MAX_SITES];  // ancestor dofs of the site's body
   double gravity[3];
   double rq[OSC_KIN_MAX_BODIES][9];          // body_quat as a rotation (row-major)
   double pos[OSC_KIN_MAX_BODIES][3];
@@ -88,6 +91,13 @@ struct alignas(16) KinDev {   // alignas: sizeof % 16 == 0 (16-byte LDS staging)
 };
 
 constexpr int even(int a) { return (a + 1) & ~1; }
+
+// Diagnostic builds only (tools/kin_ablate.sh): -DOSC_KIN_STOP=k ends the kernel before stage k.
+#ifdef OSC_KIN_STOP
+#define KIN_STOP(k) do { if ((k) == OSC_KIN_STOP) return; } while (0)
+#else
+#define KIN_STOP(k) do {} while (0)
+#endif
 
 struct EnvLayout {   // per-env LDS layout in doubles
   int q, body, dof, site, size;
@@ -127,7 +137,7 @@ __device__ __forceinline__ void inertia_mul(double m, const double* h, const dou
 // Forward pass for body b (its parent's state is final): frame, velocity, bias acceleration,
 // spatial inertia and the body's own RNEA force.  Writes the body's LDS state.
 __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
-                             int b) {
+                             int b, double s, double c) {
   double R[9], x[3], w[3], vo[3], al[3], ao[3];
   const int jt = K->jtype[b];
   const double* q = E + lay.q;
@@ -183,8 +193,6 @@ __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
         anc[i] = x[i] + Rb[3 * i] * jp[0] + Rb[3 * i + 1] * jp[1] + Rb[3 * i + 2] * jp[2];
         a[i] = Rb[3 * i] * u[0] + Rb[3 * i + 1] * u[1] + Rb[3 * i + 2] * u[2];
       }
-      double s, c;
-      sincos(q[K->qadr[b]], &s, &c);
       // Rodrigues in the body frame: Raa = c I + s [u]x + (1 - c) u u'
       const double t = 1.0 - c;
       const double Ra[9] = {c + t * u[0] * u[0], t * u[0] * u[1] - s * u[2], t * u[0] * u[2] + s * u[1],
@@ -219,7 +227,25 @@ __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
       }
     }
   }
-  // spatial inertia about the world origin: IO = R Ib R' + m (|c|^2 I - c c'), h = m c
+  double* B = E + lay.body + kBodyStride * b;
+  for (int i = 0; i < 9; ++i) B[B_R + i] = R[i];
+  for (int i = 0; i < 3; ++i) {
+    B[B_X + i] = x[i]; B[B_W + i] = w[i]; B[B_VO + i] = vo[i];
+    B[B_AL + i] = al[i]; B[B_AO + i] = ao[i];
+  }
+}
+
+// Body b's spatial inertia about the world origin and its own RNEA force, once its frame and
+// motion are in LDS (all bodies in parallel, after the level-by-level pass).
+__device__ void body_dynamics(const KinDev* K, double* E, const EnvLayout& lay, int b) {
+  double* B = E + lay.body + kBodyStride * b;
+  double R[9], x[3], w[3], vo[3], al[3], ao[3];
+  for (int i = 0; i < 9; ++i) R[i] = B[B_R + i];
+  for (int i = 0; i < 3; ++i) {
+    x[i] = B[B_X + i]; w[i] = B[B_W + i]; vo[i] = B[B_VO + i];
+    al[i] = B[B_AL + i]; ao[i] = B[B_AO + i];
+  }
+  // IO = R Ib R' + m (|c|^2 I - c c'), h = m c
   const double m = K->mass[b];
   const double* ip = K->ipos[b];
   const double* ib = K->ib[b];
@@ -252,11 +278,8 @@ __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
   cross(w, ln, t1);
   cross(vo, lf, t2);
   cross(w, lf, t3);
-  double* B = E + lay.body + kBodyStride * b;
-  for (int i = 0; i < 9; ++i) B[B_R + i] = R[i];
   for (int i = 0; i < 3; ++i) {
-    B[B_X + i] = x[i]; B[B_W + i] = w[i]; B[B_VO + i] = vo[i];
-    B[B_AL + i] = al[i]; B[B_AO + i] = ao[i]; B[B_H + i] = h[i];
+    B[B_H + i] = h[i];
     B[B_F + i] = n1[i] + t1[i] + t2[i];
     B[B_F + 3 + i] = f1[i] + t3[i];
   }
@@ -295,13 +318,22 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
   for (int i = l; i < nv; i += kRow) E[lay.q + nq + i] = qvel[static_cast<size_t>(env) * nv + i];
   wave_sync();
 
+  KIN_STOP(0);
   // ---- stage 1: forward pass, level by level (lane = body) --------------------------------
+  // Every hinge's sin / cos up front (all lanes at once), so the level loop -- whose body
+  // executes once per level -- carries no libm call; the inertia / force work, which needs no
+  // parent data, runs once for all bodies after it.
   const int my_depth = (l < nb) ? K->depth[l] : -1;
+  double sn = 0.0, cs = 1.0;
+  if (l < nb && K->jtype[l] == OSC_KIN_JOINT_HINGE) sincos(E[lay.q + K->qadr[l]], &sn, &cs);
   for (int L = 0; L < nd; ++L) {
-    if (my_depth == L) body_forward(K, E, lay, l);
+    if (my_depth == L) body_forward(K, E, lay, l, sn, cs);
     wave_sync();
   }
+  if (l < nb) body_dynamics(K, E, lay, l);
+  wave_sync();
 
+  KIN_STOP(1);
   // ---- stage 2: backward pass: subtree composite inertia and force ------------------------
   for (int L = nd - 2; L >= 0; --L) {
     if (my_depth == L) {
@@ -320,6 +352,7 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
     wave_sync();
   }
 
+  KIN_STOP(2);
   // ---- stage 3: dofs (lane = dof): motion subspace S, F = Ic S, C = S . f -----------------
   for (int d = l; d < nv; d += kRow) {
     const int bb = K->dof_body[d];
@@ -360,6 +393,7 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
     if (valid) gC[static_cast<size_t>(env) * nv + d] = cd;
   }
 
+  KIN_STOP(3);
   // ---- stage 4: sites (lane = site): world position, J-dot qvel ---------------------------
   for (int k = l; k < ns; k += kRow) {
     const int bb = K->site_body[k];
@@ -391,52 +425,74 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
   }
   wave_sync();
 
-  // ---- stage 5: M (lane = element, row-major): M_ij = S_lo . F_hi if related --------------
+  KIN_STOP(4);
+  // ---- stage 5: M (lane = columns l, l + 16; uniform loop over rows) -----------------------
+  // M_ij = S_lo . (Ic S_hi) for related dofs (lo = min(i, j)); lane j keeps S_j, F_j in
+  // registers, row i's S_i, F_i are row-broadcast LDS reads, relations come from per-dof masks
+  // (scalar loads).  Every store writes 16 consecutive doubles of one row.
+  const int c0 = l, c1 = l + kRow;
+  const bool v0 = c0 < nv, v1 = c1 < nv;
+  double S0[6], F0[6], S1[6], F1[6];
+  {
+    const double* D0 = E + lay.dof + kDofStride * (v0 ? c0 : 0);
+    const double* D1 = E + lay.dof + kDofStride * (v1 ? c1 : 0);
+    for (int t = 0; t < 6; ++t) {
+      S0[t] = D0[t]; F0[t] = D0[6 + t];
+      S1[t] = D1[t]; F1[t] = D1[6 + t];
+    }
+  }
   {
     double* Mo = gM + static_cast<size_t>(env) * nv * nv;
-    int i = 0, j = l;
-    while (j >= nv) { j -= nv; ++i; }
-    for (int e = l; e < nv * nv; e += kRow) {
-      const int lo = i < j ? i : j, hi = i < j ? j : i;
-      const int blo = K->dof_body[lo], bhi = K->dof_body[hi];
-      double v = 0.0;
-      if ((K->anc[bhi] >> blo) & 1u) {
-        const double* Sl = E + lay.dof + kDofStride * lo;
-        const double* Fh = E + lay.dof + kDofStride * hi + 6;
-        for (int t = 0; t < 6; ++t) v = fma(Sl[t], Fh[t], v);
-        if (i == j) v += K->arm[blo];
+    for (int i = 0; i < nv; ++i) {
+      const uint32_t rel = K->dof_relmask[i];
+      const double arm = K->dof_arm[i];
+      const double* Di = E + lay.dof + kDofStride * i;
+      double Si[6], Fi[6];
+      for (int t = 0; t < 6; ++t) {
+        Si[t] = Di[t];
+        Fi[t] = Di[6 + t];
       }
-      if (valid) Mo[e] = v;
-      j += kRow;
-      while (j >= nv) { j -= nv; ++i; }
+      auto entry = [&](int j, const double* Sj, const double* Fj) {   // branch-free
+        double up = 0.0, lo = 0.0;
+        for (int t = 0; t < 6; ++t) {
+          up = fma(Si[t], Fj[t], up);
+          lo = fma(Sj[t], Fi[t], lo);
+        }
+        const double v = (i <= j ? up : lo) + (i == j ? arm : 0.0);
+        return ((rel >> j) & 1u) ? v : 0.0;
+      };
+      const double m0 = entry(c0, S0, F0);
+      const double m1 = entry(c1, S1, F1);
+      if (valid && v0) Mo[i * nv + c0] = m0;
+      if (valid && v1) Mo[i * nv + c1] = m1;
     }
   }
 
-  // ---- stage 6: J (lane = element, row-major over [Jp rows; Jr rows]) ---------------------
+  KIN_STOP(5);
+  // ---- stage 6: J (lane = columns l, l + 16; uniform loop over sites) ---------------------
+  // column c of site k (c an ancestor dof of the site's body): Jr = S_c.w, Jp = S_c.v +
+  // S_c.w x x_k; rows 3k..3k+2 (Jp) and 3ns+3k.. (Jr).
   {
     double* Jo = gJ + static_cast<size_t>(env) * 6 * ns * nv;
-    const int nrow = 6 * ns;
-    int r = 0, c = l;
-    while (c >= nv) { c -= nv; ++r; }
-    for (int e = l; e < nrow * nv; e += kRow) {
-      const bool rot = r >= 3 * ns;
-      const int rr = rot ? r - 3 * ns : r;
-      const int k = rr / 3, comp = rr - 3 * k;
-      const int bk = K->site_body[k], bc = K->dof_body[c];
-      double v = 0.0;
-      if ((K->anc[bk] >> bc) & 1u) {
-        const double* S = E + lay.dof + kDofStride * c;
-        if (rot) {
-          v = S[comp];
-        } else {
-          const double* xk = E + lay.site + 3 * k;
-          const int c1 = comp == 2 ? 0 : comp + 1, c2 = comp == 0 ? 2 : comp - 1;
-          v = S[3 + comp] + (S[c1] * xk[c2] - S[c2] * xk[c1]);
+    for (int k = 0; k < ns; ++k) {
+      const uint32_t rel = K->site_dofmask[k];
+      const double* xs = E + lay.site + 3 * k;
+      const double xk[3] = {xs[0], xs[1], xs[2]};
+      auto col = [&](int c, bool vc, const double* S) {
+        const bool r = vc && ((rel >> c) & 1u);
+        double wx[3];
+        cross(S, xk, wx);
+        for (int t = 0; t < 3; ++t) {
+          const double jp = r ? S[3 + t] + wx[t] : 0.0;
+          const double jr = r ? S[t] : 0.0;
+          if (valid && vc) {
+            Jo[(3 * k + t) * nv + c] = jp;
+            Jo[(3 * ns + 3 * k + t) * nv + c] = jr;
+          }
         }
-      }
-      if (valid) Jo[e] = v;
-      c += kRow;
-      while (c >= nv) { c -= nv; ++r; }
+      };
+      col(c0, v0, S0);
+      col(c1, v1, S1);
     }
   }
 }
@@ -563,6 +619,16 @@ int build_tables(const osc_kin_desc& d, KinDev* k) {
     for (int i = 0; i < 3; ++i) k->site_pos[s][i] = d.site_pos[s][i];
   }
   for (int i = 0; i < 3; ++i) k->gravity[i] = d.gravity[i];
+  static_assert(OSC_KIN_MAX_DOFS <= 32, "dof masks are 32-bit");
+  for (int i = 0; i < nv; ++i)
+    for (int j = 0; j < nv; ++j) {
+      const int bi = k->dof_body[i], bj = k->dof_body[j];
+      if (((k->anc[bj] >> bi) & 1u) || ((k->anc[bi] >> bj) & 1u)) k->dof_relmask[i] |= 1u << j;
+    }
+  for (int i = 0; i < nv; ++i) k->dof_arm[i] = k->arm[k->dof_body[i]];
+  for (int s = 0; s < d.nsite; ++s)
+    for (int j = 0; j < nv; ++j)
+      if ((k->anc[k->site_body[s]] >> k->dof_body[j]) & 1u) k->site_dofmask[s] |= 1u << j;
   k->nbody = d.nbody;
   k->nq = nq;
   k->nv = nv;
