@@ -315,7 +315,7 @@ def main() -> None:
                               "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
             "converged_frac": converged,
         }
-        if not args.no_front_end:
+        if world == 1 and not args.no_front_end:   # rank-local extra; N=1 only, like cpu_baseline
             line["front_end"] = front_end(args.robot, solver, nenv, args.steps, args.warmup,
                                           shard_seed(rank), stream)
         if world == 1 and not args.no_cpu:
