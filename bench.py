@@ -180,6 +180,58 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
         "converged_frac": stats.converged}), flush=True)
 
 
+def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
+    """SURVEY.md §8d warm runs: a 10-step 1 % random walk of all inputs (made on the device before
+    timing, replayed ping-pong so consecutive ticks always differ by one walk step), solved with
+    the warm state carried from tick to tick (osc_batch_solve_warm; the reference's SetWarmStart,
+    operational_space_controller.h:519-526).  Reported beside the cold headline, not as it."""
+    g = torch.Generator(device=inputs[0].device).manual_seed(seed)
+    nv = inputs[0].shape[1]
+    eye = torch.eye(nv, dtype=torch.float64, device=inputs[0].device)
+    seq = [inputs]
+    for _ in range(9):
+        new = []
+        for i, t in enumerate(seq[-1]):
+            if i == 5:                                   # contact mask: unchanged
+                new.append(t)
+                continue
+            w = t * (1.0 + 0.01 * torch.randn(t.shape, generator=g, device=t.device,
+                                              dtype=t.dtype))
+            if i == 0:                                   # M: symmetric, kept SPD
+                w = 0.5 * (w + w.transpose(1, 2)) + 1e-3 * eye
+            new.append(w.contiguous())
+        seq.append(tuple(new))
+    order = list(range(10)) + list(range(8, 0, -1))
+    warm = solver.alloc_warm_state(nenv)
+    out = solver.alloc_outputs(nenv)
+    k = 0
+    for _ in range(warmup + len(order)):                 # settle, then one untimed cycle for iters
+        solver.solve_warm_into(out, warm, *seq[order[k % len(order)]])
+        k += 1
+    torch.cuda.synchronize()
+    iters = []
+    for _ in range(len(order)):
+        solver.solve_warm_into(out, warm, *seq[order[k % len(order)]])
+        iters.append(out.iters.double().mean())
+        k += 1
+    mean_iters = float(torch.stack(iters).mean().item())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        solver.solve_warm_into(out, warm, *seq[order[k % len(order)]])
+        k += 1
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    conv = float((out.status == 0).double().mean().item())
+    return {"value": nenv / (ms * 1e-3), "unit": "solves/s", "kernel_ms": ms,
+            "mean_ipm_iters": mean_iters, "converged_frac": conv,
+            "warm_state_bytes_per_env_rw": 2 * warm.numel() * 8 // max(nenv, 1),
+            "workload": "same envs, 10-step 1 % random walk of M, C, J, b, T replayed "
+                        "ping-pong, warm state carried between ticks"}
+
+
 def baseline_config_tag(args, nenv):
     """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
     tags = {("unitree_go2", "standing", "ones", 4096): 1,
@@ -202,6 +254,8 @@ def main() -> None:
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1),
                     help="CPU baseline worker processes (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-warm", action="store_true",
+                    help="skip the warm-start (random-walk) timing reported beside the headline")
     ap.add_argument("--no-front-end", action="store_true",
                     help="skip the kinematics front-end timing (reported beside the headline)")
     ap.add_argument("--mask-redraw", type=int, default=0,
@@ -315,6 +369,9 @@ def main() -> None:
                               "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
             "converged_frac": converged,
         }
+        if world == 1 and not args.no_warm:
+            line["warm"] = warm_ticks(solver, inputs, nenv, args.steps, args.warmup,
+                                      shard_seed(rank) + 7, stream)
         if world == 1 and not args.no_front_end:   # rank-local extra; N=1 only, like cpu_baseline
             line["front_end"] = front_end(args.robot, solver, nenv, args.steps, args.warmup,
                                           shard_seed(rank), stream)

@@ -146,6 +146,26 @@ int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double
                               double* tau, double* x, int32_t* status, int32_t* iters,
                               const void* workspace, size_t workspace_bytes, void* stream);
 
+/* Warm start across control ticks -- the reference's OsqpSolver::SetWarmStart with the previous
+ * tick's primal/dual solution (operational_space_controller.h:519-526).  `warm_state` is a
+ * caller-owned DEVICE buffer of osc_warm_state_bytes(model, nenv) bytes (per env: [valid flag |
+ * y | lambda | contact mask] of the interior point), zero-filled before the first tick.  An env
+ * starts cold when its state is not valid (zero-filled, or the last solve hit NaN), when its
+ * contact mask differs from the state's (a contact-mode switch changes the QP's rows), or when
+ * it has no inequality rows.  Each call reads the state and writes this tick's solution back.
+ * Results agree with the cold solve to the solve's tolerance; the iteration count drops when
+ * consecutive ticks are close. */
+int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
+int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
+                         const double* M, const double* C, const double* J, const double* b,
+                         const double* T, const double* contact_mask,
+                         double* tau, double* x, int32_t* status, int32_t* iters,
+                         double* warm_state, void* workspace, size_t workspace_bytes, void* stream);
+int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
+                                   const double* contact_mask, double* tau, double* x,
+                                   int32_t* status, int32_t* iters, double* warm_state,
+                                   const void* workspace, size_t workspace_bytes, void* stream);
+
 /* Human-readable name of an osc_status. */
 const char* osc_status_string(int status);
 

@@ -64,6 +64,7 @@ struct DevParams {
   double w_reg;
   double eps_mu;
   double inf_thresh;
+  double warm_delta;                 // warm start: slacks / multipliers floored at this value
   int32_t max_iter;
 };
 
@@ -96,6 +97,11 @@ struct Dims {
   static constexpr int W_HR = W_U + NU * NY1P;
   static constexpr int W_X = W_HR + even(NY * NY);
   static constexpr int WS = W_X + NB * NY1P;
+  // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
+  static constexpr int WW_Y = 2;
+  static constexpr int WW_L = WW_Y + even(NY);
+  static constexpr int WW_M = WW_L + NRL * 16;     // contact mask the state was solved with
+  static constexpr int WW = WW_M + even(NC);
 
   // ---- setup-kernel LDS (doubles).  R1/R2 are reused between phases.  Every matrix that the
   // 2x2-tiled products read by column pairs (A = [J | e | 0], X, U, T1) has an even row stride,
@@ -833,7 +839,7 @@ template <class D, bool SMALL>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
-    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters) {
+    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
   constexpr bool HRL = SMALL && hr_fits_lds<D>();
@@ -1123,10 +1129,49 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   double rp[NRL];
 #pragma unroll
   for (int t = 0; t < NRL; ++t) rp[t] = 0.0;
-  for (int it = -1;; ++it) {
+  // Warm start (the reference's OsqpSolver::SetWarmStart, operational_space_controller.h:525):
+  // an env whose warm state is valid starts from the previous tick's y and lambda, with the
+  // slacks s = max(h - G y, delta) and lambda = max(lambda_prev, delta) (rows active now but not
+  // before start at delta).  A wave whose four envs are all warm skips the least-squares initial
+  // point; otherwise it runs it and the warm rows override it at iteration 0.  An env without
+  // active rows always starts cold (its initial point is then the exact optimum).
+  // (nothing warm-related stays live across the loop but one lane mask: the 2-wave variant has
+  // no registers to spare)
+  // A contact-mode switch (mask differs from the state's) changes the QP's rows: start cold.
+  bool warm = false;
+  if (gwarm != nullptr) {
+    const double* w0 = gwarm + static_cast<size_t>(env) * D::WW;
+    const double same = (l >= NC || w0[D::WW_M + l] == sMask[l]) ? 1.0 : 0.0;
+    warm = row_min(same) == 1.0 && w0[0] == 1.0 && m_act > 0.0;
+  }
+  const bool any_warm = __ballot(warm) != 0;
+  const bool all_warm = __ballot(!warm) == 0;
+  for (int it = all_warm ? 0 : -1;; ++it) {
     STAMP_BEGIN();
     const bool init = it < 0;
     double mu = 0.0;
+    if (it == 0 && any_warm) {
+      const double* wst = gwarm + static_cast<size_t>(env) * D::WW;
+      if (warm) {
+        y0 = wst[D::WW_Y + j0];
+        y1 = v1 ? wst[D::WW_Y + j1] : 0.0;
+        sVy[j0] = y0;
+        if (v1) sVy[j1] = y1;
+      }
+      wave_sync();
+      uv_product(sVy);
+      wave_sync();
+      if (warm) {
+        const double dlt = P->warm_delta;
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          const double gy = Gv(sVy, t);
+          const double wl = wst[D::WW_L + l + kRow * t];
+          s[t] = act[t] ? fmax(h[t] - gy, dlt) : 1.0;
+          lam[t] = act[t] ? fmax(wl, dlt) : 0.0;
+        }
+      }
+    }
     if (!init) {
       double cs = 0.0;
 #pragma unroll
@@ -1366,6 +1411,15 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       if (gstatus) gstatus[env] = st;
       if (giters) giters[env] = it_done;
     }
+    if (gwarm != nullptr) {   // this tick's y and lambda for the next one (NaN: next tick cold)
+      double* wo = gwarm + static_cast<size_t>(env) * D::WW;
+      wo[D::WW_Y + j0] = y0;
+      if (v1) wo[D::WW_Y + j1] = y1;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) wo[D::WW_L + l + kRow * t] = lam[t];
+      if (l < NC) wo[D::WW_M + l] = sMask[l];
+      if (l == 0) wo[0] = (st == OSC_SOLVE_NUMERICAL) ? 0.0 : 1.0;
+    }
   }
 }
 
@@ -1379,6 +1433,14 @@ KernelId select_kernel(const osc_model_desc& d) {
   if (d.nv == Walter::NV && d.nu == Walter::NU && d.nc == Walter::NC && d.ns == Walter::NS)
     return K_WALTER;
   return K_NONE;
+}
+
+int ww_doubles(KernelId k) {
+  switch (k) {
+    case K_GO2: return Go2::WW;
+    case K_WALTER: return Walter::WW;
+    default: return 0;
+  }
 }
 
 int ws_doubles(KernelId k) {
@@ -1441,6 +1503,7 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.eps_mu = d.eps_mu;
   hp.inf_thresh = thresh;
   hp.max_iter = d.max_iter;
+  hp.warm_delta = 0.1;   // tools/ipm_model.py warm-start study: 1 % random walk, Go2 mean 11.1 -> 7.4
 
   osc_model* m = new (std::nothrow) osc_model;
   if (!m) return OSC_ERR_DEVICE;
@@ -1500,7 +1563,7 @@ enum Stage : unsigned { kAssemble = 1u, kInteriorPoint = 2u, kBoth = 3u };
 template <class D>
 void launch_t(const osc_model* model, int32_t nenv, const double* M, const double* C,
               const double* J, const double* b, const double* T, const double* mask, double* tau,
-              double* x, int32_t* status, int32_t* iters, double* ws, hipStream_t s,
+              double* x, int32_t* status, int32_t* iters, double* ws, double* warm, hipStream_t s,
               unsigned stages) {
   if (stages & kAssemble)
     hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
@@ -1511,10 +1574,10 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
     if (nenv <= model->small_batch_max)
       hipLaunchKernelGGL((osc_ipm_kernel<D, true>), dim3(nb), dim3(kWave), 0, s, model->dparams,
-                         nenv, mask, ws, tau, x, status, iters);
+                         nenv, mask, ws, tau, x, status, iters, warm);
     else
       hipLaunchKernelGGL((osc_ipm_kernel<D, false>), dim3(nb), dim3(kWave), 0, s, model->dparams,
-                         nenv, mask, ws, tau, x, status, iters);
+                         nenv, mask, ws, tau, x, status, iters, warm);
   }
 }
 
@@ -1523,7 +1586,7 @@ bool misaligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u)
 int launch(const osc_model* model, int32_t nenv, const double* M, const double* C, const double* J,
            const double* b, const double* T, const double* contact_mask, double* tau, double* x,
            int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes,
-           void* stream, unsigned stages) {
+           void* stream, unsigned stages, double* warm = nullptr) {
   if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
   if (nenv == 0) return OSC_OK;
   if (!contact_mask || misaligned16(contact_mask)) return OSC_ERR_INVALID_ARGUMENT;
@@ -1550,10 +1613,11 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
   int rc = OSC_OK;
   switch (model->kid) {
     case K_GO2:
-      launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s, stages);
+      launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, warm, s,
+                    stages);
       break;
     case K_WALTER:
-      launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, s,
+      launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, warm, s,
                        stages);
       break;
     default:
@@ -1581,6 +1645,33 @@ extern "C" int osc_batch_assemble(const osc_model* model, int32_t nenv, const do
                                   size_t workspace_bytes, void* stream) {
   return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
                 workspace, workspace_bytes, stream, kAssemble);
+}
+
+extern "C" int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes) {
+  if (!model || !bytes || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+  *bytes = sizeof(double) * static_cast<size_t>(ww_doubles(model->kid)) * static_cast<size_t>(nenv);
+  return OSC_OK;
+}
+
+extern "C" int osc_batch_solve_warm(const osc_model* model, int32_t nenv, const double* M,
+                                    const double* C, const double* J, const double* b,
+                                    const double* T, const double* contact_mask, double* tau,
+                                    double* x, int32_t* status, int32_t* iters, double* warm_state,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  if (!warm_state) return OSC_ERR_INVALID_ARGUMENT;
+  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
+                workspace_bytes, stream, kBoth, warm_state);
+}
+
+extern "C" int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
+                                              const double* contact_mask, double* tau, double* x,
+                                              int32_t* status, int32_t* iters, double* warm_state,
+                                              const void* workspace, size_t workspace_bytes,
+                                              void* stream) {
+  if (!warm_state) return OSC_ERR_INVALID_ARGUMENT;
+  return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, nullptr, contact_mask, tau, x,
+                status, iters, const_cast<void*>(workspace), workspace_bytes, stream,
+                kInteriorPoint, warm_state);
 }
 
 extern "C" int osc_batch_solve_assembled(const osc_model* model, int32_t nenv,

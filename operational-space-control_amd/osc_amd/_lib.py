@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_kin_desc_from_json", "osc_kin_model_create",
                     "osc_kin_model_create_from_json", "osc_kin_model_destroy",
                     "osc_kin_model_dims", "osc_batch_kinematics", "osc_state_to_qpos",
-                    "osc_qpos_workspace_bytes", "osc_batch_solve_qpos")
+                    "osc_qpos_workspace_bytes", "osc_batch_solve_qpos",
+                    "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -114,6 +115,12 @@ def lib() -> ctypes.CDLL:
     L.osc_pd_base_targets.restype = ctypes.c_int
     L.osc_contact_mask_from_contacts.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, vp]
     L.osc_contact_mask_from_contacts.restype = ctypes.c_int
+    L.osc_warm_state_bytes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t)]
+    L.osc_warm_state_bytes.restype = ctypes.c_int
+    L.osc_batch_solve_warm.argtypes = [vp, i32] + [vp] * 12 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_warm.restype = ctypes.c_int
+    L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 7 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_assembled_warm.restype = ctypes.c_int
     kp = ctypes.POINTER(OscKinDesc)
     L.osc_kin_desc_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, kp]
     L.osc_kin_desc_from_json.restype = ctypes.c_int

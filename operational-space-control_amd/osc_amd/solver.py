@@ -132,6 +132,44 @@ class OSCBatchSolver:
             raise _lib.OSCError("osc_batch_solve_assembled", rc)
         return out
 
+    def alloc_warm_state(self, nenv: int) -> torch.Tensor:
+        """Zero-filled warm state (osc_warm_state_bytes): every env starts cold on its first tick."""
+        nb = ctypes.c_size_t()
+        rc = _lib.lib().osc_warm_state_bytes(self._h, nenv, ctypes.byref(nb))
+        if rc != 0:
+            raise _lib.OSCError("osc_warm_state_bytes", rc)
+        return torch.zeros((max(nb.value // 8, 2),), dtype=torch.float64, device=self.device)
+
+    def solve_warm_into(self, out: SolveResult, warm: torch.Tensor, M, C, J, b, T, mask,
+                        stream=None) -> SolveResult:
+        """osc_batch_solve_warm: as solve_into, starting from (and updating) `warm`, the previous
+        tick's solution (the reference's SetWarmStart, operational_space_controller.h:519-526)."""
+        nenv = out.tau.shape[0]
+        s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = _lib.lib().osc_batch_solve_warm(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
+                                             ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
+                                             ptr(out.iters), ptr(warm), ptr(out.workspace),
+                                             ctypes.c_size_t(0 if out.workspace is None else
+                                                             out.workspace.numel() * 8),
+                                             ctypes.c_void_p(s))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_solve_warm", rc)
+        return out
+
+    def solve_assembled_warm_into(self, out: SolveResult, warm: torch.Tensor, mask,
+                                  stream=None) -> SolveResult:
+        nenv = out.tau.shape[0]
+        s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = _lib.lib().osc_batch_solve_assembled_warm(
+            self._h, nenv, ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status), ptr(out.iters),
+            ptr(warm), ptr(out.workspace), ctypes.c_size_t(out.workspace.numel() * 8),
+            ctypes.c_void_p(s))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_solve_assembled_warm", rc)
+        return out
+
     def prepare(self, M, C, J, b, T, mask):
         d = self.dims
         nenv = int(M.shape[0])
