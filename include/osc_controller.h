@@ -25,7 +25,8 @@
  * Per tick (the reference's control_loop body, :556-574), under the mutex:
  *   (a) pack qpos/qvel -> one host->device copy -> osc_batch_solve_qpos(nenv = 1), or
  *   (b) kinematics(state) -> host->device copy -> osc_batch_solve(nenv = 1),
- * then torque_command = x[nv : nv+nu].
+ * then torque_command = x[nv : nv+nu].  Every tick is warm-started from the previous one (the
+ * reference's OsqpSolver::SetWarmStart, :519-526; osc_batch_solve_warm).
  * step() runs one such tick synchronously (for callers without the thread, and tests).
  */
 #ifndef OSC_CONTROLLER_H_
@@ -157,6 +158,8 @@ class OperationalSpaceController {
   int32_t* d_info_ = nullptr;       // status | iters
   void* d_ws_ = nullptr;
   size_t ws_bytes_ = 0;
+  double* d_warm_ = nullptr;        // interior-point warm state carried between ticks
+  size_t warm_bytes_ = 0;
   std::vector<double> h_in_;
 };
 

@@ -113,6 +113,12 @@ int osc_batch_solve_qpos(const osc_model* model, const osc_kin_model* kin, int32
                          const double* qpos, const double* qvel, const double* T,
                          const double* contact_mask, double* tau, double* x, int32_t* status,
                          int32_t* iters, void* workspace, size_t workspace_bytes, void* stream);
+/* Same, warm-started from / updating `warm_state` (osc_batch.h, osc_batch_solve_warm). */
+int osc_batch_solve_qpos_warm(const osc_model* model, const osc_kin_model* kin, int32_t nenv,
+                              const double* qpos, const double* qvel, const double* T,
+                              const double* contact_mask, double* tau, double* x,
+                              int32_t* status, int32_t* iters, double* warm_state,
+                              void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -121,7 +121,10 @@ Status OperationalSpaceController::initialize_optimization() {
       hipMalloc(reinterpret_cast<void**>(&d_in_), in_doubles * sizeof(double)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&d_out_), (even(nu_) + even(n_)) * sizeof(double)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&d_info_), 2 * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&d_ws_, ws_bytes_) != hipSuccess) {
+      hipMalloc(&d_ws_, ws_bytes_) != hipSuccess ||
+      osc_warm_state_bytes(model_, 1, &warm_bytes_) != OSC_OK ||
+      hipMalloc(reinterpret_cast<void**>(&d_warm_), warm_bytes_) != hipSuccess ||
+      hipMemset(d_warm_, 0, warm_bytes_) != hipSuccess) {
     stream_ = stream;
     release_device();
     return InternalError("device allocation failed");
@@ -224,11 +227,11 @@ Status OperationalSpaceController::tick_gpu_kinematics_locked() {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (hipMemcpyAsync(d_in_, h, off * sizeof(double), hipMemcpyHostToDevice, stream) != hipSuccess)
     return InternalError("host to device copy failed");
-  return from_osc(osc_batch_solve_qpos(model_, kin_, 1, d_in_, d_in_ + (qvel - h),
-                                       d_in_ + (T - h), d_in_ + (mask - h), d_out_,
-                                       d_out_ + even(nu_), d_info_, d_info_ + 1, d_ws_, ws_bytes_,
-                                       stream_),
-                  "osc_batch_solve_qpos");
+  return from_osc(osc_batch_solve_qpos_warm(model_, kin_, 1, d_in_, d_in_ + (qvel - h),
+                                            d_in_ + (T - h), d_in_ + (mask - h), d_out_,
+                                            d_out_ + even(nu_), d_info_, d_info_ + 1, d_warm_,
+                                            d_ws_, ws_bytes_, stream_),
+                  "osc_batch_solve_qpos_warm");
 }
 
 // The body of the reference's control_loop (:556-574), caller holds the mutex.
@@ -266,9 +269,11 @@ Status OperationalSpaceController::tick_locked() {
     return InternalError("host to device copy failed");
   double* d_tau = d_out_;
   double* d_x = d_out_ + even(nu_);
-  st = from_osc(osc_batch_solve(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4], dptr[5],
-                                d_tau, d_x, d_info_, d_info_ + 1, d_ws_, ws_bytes_, stream_),
-                "osc_batch_solve");
+  // warm-started from the previous tick, as the reference's SetWarmStart (:519-526)
+  st = from_osc(osc_batch_solve_warm(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4],
+                                     dptr[5], d_tau, d_x, d_info_, d_info_ + 1, d_warm_, d_ws_,
+                                     ws_bytes_, stream_),
+                "osc_batch_solve_warm");
   if (!st.ok()) return st;
   return fetch_outputs_locked();
 }
@@ -318,6 +323,8 @@ void OperationalSpaceController::release_device() {
   if (d_out_) (void)hipFree(d_out_);
   if (d_info_) (void)hipFree(d_info_);
   if (d_ws_) (void)hipFree(d_ws_);
+  if (d_warm_) (void)hipFree(d_warm_);
+  d_warm_ = nullptr;
   if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
   if (model_) (void)osc_model_destroy(model_);
   if (kin_) (void)osc_kin_model_destroy(kin_);

@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_kin_model_create_from_json", "osc_kin_model_destroy",
                     "osc_kin_model_dims", "osc_batch_kinematics", "osc_state_to_qpos",
                     "osc_qpos_workspace_bytes", "osc_batch_solve_qpos",
-                    "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm")
+                    "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm",
+                    "osc_batch_solve_qpos_warm")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -142,6 +143,8 @@ def lib() -> ctypes.CDLL:
     L.osc_qpos_workspace_bytes.restype = ctypes.c_int
     L.osc_batch_solve_qpos.argtypes = [vp, vp, i32] + [vp] * 9 + [ctypes.c_size_t, vp]
     L.osc_batch_solve_qpos.restype = ctypes.c_int
+    L.osc_batch_solve_qpos_warm.argtypes = [vp, vp, i32] + [vp] * 10 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_qpos_warm.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -157,6 +157,19 @@ class KinematicsBatch:
             raise _lib.OSCError("osc_batch_solve_qpos", rc)
         return out
 
+    def solve_warm_into(self, solver, out, warm, qpos, qvel, T, mask, workspace, stream=None):
+        """osc_batch_solve_qpos_warm: the tick from joint states, warm-started from `warm`."""
+        nenv = out.tau.shape[0]
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = _lib.lib().osc_batch_solve_qpos_warm(
+            solver._h, self._h, nenv, ptr(qpos), ptr(qvel), ptr(T), ptr(mask), ptr(out.tau),
+            ptr(out.x), ptr(out.status), ptr(out.iters), ptr(warm), ptr(workspace),
+            ctypes.c_size_t(0 if workspace is None else workspace.numel() * 8),
+            ctypes.c_void_p(self._stream(stream, self.device)))
+        if rc != 0:
+            raise _lib.OSCError("osc_batch_solve_qpos_warm", rc)
+        return out
+
     def solve(self, solver, qpos, qvel, T, mask, want_x: bool = False):
         d = solver.dims
         nenv = int(qpos.shape[0])

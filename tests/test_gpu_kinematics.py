@@ -136,3 +136,31 @@ def test_solve_from_joint_states(gpu, robot):
         args = (M, C, J, b, T[e], mask[e])
         tr = torque(model, solve_exact(model, build_qp(model, *args), M, C, J).x)
         assert np.abs(tau[e] - tr).max() / max(np.abs(tr).max(), 1.0) <= 1e-5, e
+
+
+def test_warm_solve_from_joint_states(gpu):
+    """osc_batch_solve_qpos_warm == osc_batch_kinematics + osc_batch_solve_warm, bitwise, over
+    three ticks of a small joint-space walk (warm state carried)."""
+    from osc_amd.solver import OSCBatchSolver
+    tree = load_tree("unitree_go2")
+    kb = KinematicsBatch(tree=tree)
+    solver = OSCBatchSolver("unitree_go2")
+    nenv = 16
+    qpos, qvel = random_states(tree, nenv, 5, joint_range=0.5)
+    rng = np.random.default_rng(5)
+    T = np.zeros((nenv, 5, 6))
+    T[:, 0] = 10.0 * rng.standard_normal((nenv, 6))
+    mask = np.ones((nenv, 4))
+    wa, wb = solver.alloc_warm_state(nenv), solver.alloc_warm_state(nenv)
+    oa, ob = solver.alloc_outputs(nenv), solver.alloc_outputs(nenv)
+    ws = torch.empty((kb.workspace_bytes(solver, nenv) // 8 + 2,), dtype=torch.float64, device=gpu)
+    Td, md = torch.from_numpy(T).to(gpu), torch.from_numpy(mask).to(gpu)
+    for k in range(3):
+        qp = torch.from_numpy(qpos + 0.01 * k).to(gpu)
+        qv = torch.from_numpy(qvel).to(gpu)
+        kb.solve_warm_into(solver, oa, wa, qp, qv, Td, md, ws)
+        kk = kb.compute(qp, qv, want_sites=False)
+        solver.solve_warm_into(ob, wb, kk.M, kk.C, kk.J, kk.b, Td, md)
+        torch.cuda.synchronize()
+        assert torch.equal(oa.tau, ob.tau) and torch.equal(wa, wb)
+        assert (oa.status.cpu().numpy() == 0).all()
