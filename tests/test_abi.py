@@ -119,3 +119,28 @@ def test_kin_desc_errors():
         h = ct.c_void_p()
         assert L.osc_kin_model_create(ct.byref(d), ct.byref(h)) == 1
     assert L.osc_batch_kinematics(None, 1, *([None] * 7), None) == 1
+
+
+@pytest.mark.parametrize("text", ['{"bodies": [', '{"gravity": [0, 0], "bodies": [], "sites": []}',
+                                  '{"gravity": [0, 0, -9.81], "bodies": [{"parent": -1}], "sites": []}',
+                                  '[1, 2, 3]', ''])
+def test_kin_desc_from_json_rejects_malformed(tmp_path, text):
+    f = tmp_path / "tree.json"
+    f.write_text(text)
+    with pytest.raises(_lib.OSCError) as e:
+        _lib.kin_desc_from_json(None, str(f))
+    assert e.value.code == 3   # OSC_ERR_IO
+
+
+def test_kin_desc_joint_strings_and_defaults(tmp_path):
+    import json
+    from kin_trees import random_tree
+    t = random_tree(3, nbody=4, nsite=2)
+    for b in t["bodies"][1:]:                  # optional keys may be omitted
+        b.pop("armature"); b.pop("jnt_pos")
+    f = tmp_path / "tree.json"
+    f.write_text(json.dumps(t))
+    d = _lib.kin_desc_from_json(None, str(f))
+    assert d.nbody == 4 and d.nsite == 2
+    assert list(d.jnt_type[:4]) == [{"free": 0, "hinge": 3, "none": -1}[b["joint"]] for b in t["bodies"]]
+    assert all(d.armature[i] == 0.0 for i in range(1, 4))
