@@ -1,23 +1,23 @@
 #!/bin/bash
 # Stage ablation of the kinematics kernel: builds libosc_batch.so variants that stop before
-# stage k (k = 0..5) under tools/build/kin_stop<k>/ (run here, cross-compiled), then on the GPU
+# stage k (k = 0..5) under operational-space-control_amd/lib/ablate/kin_stop<k>/ (run here, cross-compiled), then on the GPU
 #   for k in 0 1 2 3 4 5 full; do OSC_LIB_PATH=... python tools/kin_bench.py; done
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/operational-space-control_amd/csrc
 if [ "$1" = "build" ]; then
   for k in 0 1 2 3 4 5; do
-    mkdir -p $R/tools/build/kin_stop$k
+    mkdir -p $R/operational-space-control_amd/lib/ablate/kin_stop$k
     /opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -fPIC -shared -DOSC_KIN_STOP=$k \
       -I $R/include $C/osc_batch.hip $C/osc_model.cpp $C/osc_producers.hip $C/osc_kinematics.hip \
-      -o $R/tools/build/kin_stop$k/libosc_batch.so &
+      -o $R/operational-space-control_amd/lib/ablate/kin_stop$k/libosc_batch.so &
   done
   wait
   exit 0
 fi
 for k in 0 1 2 3 4 5; do
   echo "stop before stage $k"
-  OSC_LIB_PATH=$R/tools/build/kin_stop$k/libosc_batch.so timeout -k 10 60 python $R/tools/kin_bench.py --steps 20
+  OSC_LIB_PATH=$R/operational-space-control_amd/lib/ablate/kin_stop$k/libosc_batch.so timeout -k 10 60 python $R/tools/kin_bench.py --steps 20
 done
 echo "full"
 timeout -k 10 60 python $R/tools/kin_bench.py --steps 20
