@@ -160,10 +160,12 @@ int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
                          const double* M, const double* C, const double* J, const double* b,
                          const double* T, const double* contact_mask,
                          double* tau, double* x, int32_t* status, int32_t* iters,
-                         double* warm_state, void* workspace, size_t workspace_bytes, void* stream);
+                         double* warm_state, size_t warm_state_bytes,
+                         void* workspace, size_t workspace_bytes, void* stream);
 int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
                                    const double* contact_mask, double* tau, double* x,
-                                   int32_t* status, int32_t* iters, double* warm_state,
+                                   int32_t* status, int32_t* iters,
+                                   double* warm_state, size_t warm_state_bytes,
                                    const void* workspace, size_t workspace_bytes, void* stream);
 
 /* Human-readable name of an osc_status. */

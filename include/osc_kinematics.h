@@ -117,7 +117,8 @@ int osc_batch_solve_qpos(const osc_model* model, const osc_kin_model* kin, int32
 int osc_batch_solve_qpos_warm(const osc_model* model, const osc_kin_model* kin, int32_t nenv,
                               const double* qpos, const double* qvel, const double* T,
                               const double* contact_mask, double* tau, double* x,
-                              int32_t* status, int32_t* iters, double* warm_state,
+                              int32_t* status, int32_t* iters,
+                              double* warm_state, size_t warm_state_bytes,
                               void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus

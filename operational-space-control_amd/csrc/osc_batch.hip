@@ -1653,12 +1653,23 @@ extern "C" int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t
   return OSC_OK;
 }
 
+namespace {
+// true when the warm-state buffer is usable: non-null and at least osc_warm_state_bytes
+bool warm_small(const osc_model* model, int32_t nenv, const double* warm, size_t bytes) {
+  size_t need = 0;
+  if (!model || !warm || osc_warm_state_bytes(model, nenv < 0 ? 0 : nenv, &need) != OSC_OK)
+    return false;
+  return bytes >= need;
+}
+}  // namespace
+
 extern "C" int osc_batch_solve_warm(const osc_model* model, int32_t nenv, const double* M,
                                     const double* C, const double* J, const double* b,
                                     const double* T, const double* contact_mask, double* tau,
                                     double* x, int32_t* status, int32_t* iters, double* warm_state,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
-  if (!warm_state) return OSC_ERR_INVALID_ARGUMENT;
+                                    size_t warm_state_bytes, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  if (!warm_small(model, nenv, warm_state, warm_state_bytes)) return OSC_ERR_INVALID_ARGUMENT;
   return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
                 workspace_bytes, stream, kBoth, warm_state);
 }
@@ -1666,9 +1677,9 @@ extern "C" int osc_batch_solve_warm(const osc_model* model, int32_t nenv, const 
 extern "C" int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
                                               const double* contact_mask, double* tau, double* x,
                                               int32_t* status, int32_t* iters, double* warm_state,
-                                              const void* workspace, size_t workspace_bytes,
-                                              void* stream) {
-  if (!warm_state) return OSC_ERR_INVALID_ARGUMENT;
+                                              size_t warm_state_bytes, const void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+  if (!warm_small(model, nenv, warm_state, warm_state_bytes)) return OSC_ERR_INVALID_ARGUMENT;
   return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, nullptr, contact_mask, tau, x,
                 status, iters, const_cast<void*>(workspace), workspace_bytes, stream,
                 kInteriorPoint, warm_state);

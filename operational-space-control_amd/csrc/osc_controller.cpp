@@ -230,7 +230,7 @@ Status OperationalSpaceController::tick_gpu_kinematics_locked() {
   return from_osc(osc_batch_solve_qpos_warm(model_, kin_, 1, d_in_, d_in_ + (qvel - h),
                                             d_in_ + (T - h), d_in_ + (mask - h), d_out_,
                                             d_out_ + even(nu_), d_info_, d_info_ + 1, d_warm_,
-                                            d_ws_, ws_bytes_, stream_),
+                                            warm_bytes_, d_ws_, ws_bytes_, stream_),
                   "osc_batch_solve_qpos_warm");
 }
 
@@ -271,8 +271,8 @@ Status OperationalSpaceController::tick_locked() {
   double* d_x = d_out_ + even(nu_);
   // warm-started from the previous tick, as the reference's SetWarmStart (:519-526)
   st = from_osc(osc_batch_solve_warm(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4],
-                                     dptr[5], d_tau, d_x, d_info_, d_info_ + 1, d_warm_, d_ws_,
-                                     ws_bytes_, stream_),
+                                     dptr[5], d_tau, d_x, d_info_, d_info_ + 1, d_warm_,
+                                     warm_bytes_, d_ws_, ws_bytes_, stream_),
                 "osc_batch_solve_warm");
   if (!st.ok()) return st;
   return fetch_outputs_locked();

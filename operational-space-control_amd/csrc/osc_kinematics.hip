@@ -948,7 +948,8 @@ namespace {
 
 int solve_qpos(const osc_model* model, const osc_kin_model* kin, int32_t nenv, const double* qpos,
                const double* qvel, const double* T, const double* contact_mask, double* tau,
-               double* x, int32_t* status, int32_t* iters, double* warm_state, void* workspace,
+               double* x, int32_t* status, int32_t* iters, double* warm_state,
+               size_t warm_state_bytes, void* workspace,
                size_t workspace_bytes, void* stream) {
   int rc = check_pair(model, kin);
   if (rc != OSC_OK) return rc;
@@ -973,7 +974,8 @@ int solve_qpos(const osc_model* model, const osc_kin_model* kin, int32_t nenv, c
   rc = osc_batch_kinematics(kin, nenv, qpos, qvel, M, C, J, b, nullptr, stream);
   if (rc == OSC_OK)
     rc = warm_state ? osc_batch_solve_warm(model, nenv, M, C, J, b, T, contact_mask, tau, x,
-                                           status, iters, warm_state, base + L.ws, L.ws_bytes,
+                                           status, iters, warm_state, warm_state_bytes,
+                                           base + L.ws, L.ws_bytes,
                                            stream)
                     : osc_batch_solve(model, nenv, M, C, J, b, T, contact_mask, tau, x, status,
                                       iters, base + L.ws, L.ws_bytes, stream);
@@ -989,16 +991,16 @@ extern "C" int osc_batch_solve_qpos(const osc_model* model, const osc_kin_model*
                                     double* x, int32_t* status, int32_t* iters, void* workspace,
                                     size_t workspace_bytes, void* stream) {
   return solve_qpos(model, kin, nenv, qpos, qvel, T, contact_mask, tau, x, status, iters, nullptr,
-                    workspace, workspace_bytes, stream);
+                    0, workspace, workspace_bytes, stream);
 }
 
 extern "C" int osc_batch_solve_qpos_warm(const osc_model* model, const osc_kin_model* kin,
                                          int32_t nenv, const double* qpos, const double* qvel,
                                          const double* T, const double* contact_mask, double* tau,
                                          double* x, int32_t* status, int32_t* iters,
-                                         double* warm_state, void* workspace,
-                                         size_t workspace_bytes, void* stream) {
+                                         double* warm_state, size_t warm_state_bytes,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
   if (!warm_state) return OSC_ERR_INVALID_ARGUMENT;
   return solve_qpos(model, kin, nenv, qpos, qvel, T, contact_mask, tau, x, status, iters,
-                    warm_state, workspace, workspace_bytes, stream);
+                    warm_state, warm_state_bytes, workspace, workspace_bytes, stream);
 }

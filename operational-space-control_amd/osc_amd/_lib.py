@@ -118,9 +118,11 @@ def lib() -> ctypes.CDLL:
     L.osc_contact_mask_from_contacts.restype = ctypes.c_int
     L.osc_warm_state_bytes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t)]
     L.osc_warm_state_bytes.restype = ctypes.c_int
-    L.osc_batch_solve_warm.argtypes = [vp, i32] + [vp] * 12 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_warm.argtypes = [vp, i32] + [vp] * 11 + [ctypes.c_size_t, vp,
+                                                               ctypes.c_size_t, vp]
     L.osc_batch_solve_warm.restype = ctypes.c_int
-    L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 7 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 6 + [ctypes.c_size_t, vp,
+                                                                         ctypes.c_size_t, vp]
     L.osc_batch_solve_assembled_warm.restype = ctypes.c_int
     kp = ctypes.POINTER(OscKinDesc)
     L.osc_kin_desc_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, kp]
@@ -143,7 +145,8 @@ def lib() -> ctypes.CDLL:
     L.osc_qpos_workspace_bytes.restype = ctypes.c_int
     L.osc_batch_solve_qpos.argtypes = [vp, vp, i32] + [vp] * 9 + [ctypes.c_size_t, vp]
     L.osc_batch_solve_qpos.restype = ctypes.c_int
-    L.osc_batch_solve_qpos_warm.argtypes = [vp, vp, i32] + [vp] * 10 + [ctypes.c_size_t, vp]
+    L.osc_batch_solve_qpos_warm.argtypes = [vp, vp, i32] + [vp] * 9 + [ctypes.c_size_t, vp,
+                                                                      ctypes.c_size_t, vp]
     L.osc_batch_solve_qpos_warm.restype = ctypes.c_int
     _lib = L
     return L

@@ -163,7 +163,8 @@ class KinematicsBatch:
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         rc = _lib.lib().osc_batch_solve_qpos_warm(
             solver._h, self._h, nenv, ptr(qpos), ptr(qvel), ptr(T), ptr(mask), ptr(out.tau),
-            ptr(out.x), ptr(out.status), ptr(out.iters), ptr(warm), ptr(workspace),
+            ptr(out.x), ptr(out.status), ptr(out.iters), ptr(warm),
+            ctypes.c_size_t(0 if warm is None else warm.numel() * 8), ptr(workspace),
             ctypes.c_size_t(0 if workspace is None else workspace.numel() * 8),
             ctypes.c_void_p(self._stream(stream, self.device)))
         if rc != 0:

@@ -149,7 +149,9 @@ class OSCBatchSolver:
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         rc = _lib.lib().osc_batch_solve_warm(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
                                              ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
-                                             ptr(out.iters), ptr(warm), ptr(out.workspace),
+                                             ptr(out.iters), ptr(warm),
+                                             ctypes.c_size_t(0 if warm is None else warm.numel() * 8),
+                                             ptr(out.workspace),
                                              ctypes.c_size_t(0 if out.workspace is None else
                                                              out.workspace.numel() * 8),
                                              ctypes.c_void_p(s))
@@ -164,7 +166,8 @@ class OSCBatchSolver:
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         rc = _lib.lib().osc_batch_solve_assembled_warm(
             self._h, nenv, ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status), ptr(out.iters),
-            ptr(warm), ptr(out.workspace), ctypes.c_size_t(out.workspace.numel() * 8),
+            ptr(warm), ctypes.c_size_t(0 if warm is None else warm.numel() * 8),
+            ptr(out.workspace), ctypes.c_size_t(out.workspace.numel() * 8),
             ctypes.c_void_p(s))
         if rc != 0:
             raise _lib.OSCError("osc_batch_solve_assembled_warm", rc)

@@ -66,3 +66,6 @@ def test_warm_state_api_errors(gpu):
     out = solver.alloc_outputs(nenv)
     with pytest.raises(_lib.OSCError):
         solver.solve_warm_into(out, None, *args)
+    short = solver.alloc_warm_state(nenv)[:-2]          # one env's state short
+    with pytest.raises(_lib.OSCError):
+        solver.solve_warm_into(out, short, *args)
