@@ -42,3 +42,21 @@ def chain_tree(seed: int, nbody: int = 16) -> dict:
     for i, b in enumerate(t["bodies"][1:], start=1):
         b["parent"] = i - 1
     return t
+
+
+def free_body(mass=2.0, diag=(0.1, 0.2, 0.3), iquat=(1.0, 0.0, 0.0, 0.0)) -> dict:
+    """A single free body with its COM at the body origin and one site there."""
+    return dict(name="free body", gravity=[0.0, 0.0, -9.81], bodies=[dict(
+        name="b", parent=-1, pos=[0, 0, 0], quat=[1, 0, 0, 0], joint="free", axis=[0, 0, 1],
+        jnt_pos=[0, 0, 0], armature=0.0, mass=mass, ipos=[0, 0, 0], iquat=list(iquat),
+        diaginertia=list(diag))], sites=[dict(name="s", body=0, pos=[0, 0, 0])])
+
+
+def pendulum(mass=1.5, length=0.7, izz=1e-3, armature=0.05) -> dict:
+    """A point-like mass on a hinge about the world y axis, COM at -length along z, welded to the
+    world (fixed base), one site at the COM."""
+    return dict(name="pendulum", gravity=[0.0, 0.0, -9.81], bodies=[dict(
+        name="arm", parent=-1, pos=[0, 0, 0], quat=[1, 0, 0, 0], joint="hinge", axis=[0, 1, 0],
+        jnt_pos=[0, 0, 0], armature=armature, mass=mass, ipos=[0, 0, -length],
+        iquat=[1, 0, 0, 0], diaginertia=[izz, izz, izz])],
+        sites=[dict(name="bob", body=0, pos=[0, 0, -length])])

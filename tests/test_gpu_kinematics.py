@@ -12,7 +12,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 import kinematics as kin
-from kin_trees import chain_tree, random_tree
+from kin_trees import chain_tree, free_body, pendulum, random_tree
 from osc_amd.kinematics import KinematicsBatch, load_tree, random_states
 
 pytestmark = pytest.mark.gpu
@@ -164,3 +164,33 @@ def test_warm_solve_from_joint_states(gpu):
         torch.cuda.synchronize()
         assert torch.equal(oa.tau, ob.tau) and torch.equal(wa, wb)
         assert (oa.status.cpu().numpy() == 0).all()
+
+
+def test_known_answer_trees(gpu):
+    """The kernel against closed forms (tests/test_kinematics_oracle.py): a pendulum (M = m L^2 +
+    I + armature, qfrc_bias = m g L sin th, Jp, Jdot qdot) and a free body with body-frame
+    rotational dofs (M = blockdiag(m I, I_body), qfrc_bias = (m g e_z, w x I w))."""
+    from test_kinematics_oracle import free_body_known_answer, pendulum_known_answer
+    kb = KinematicsBatch(tree=pendulum())
+    th = np.array([0.3, -1.1, 2.5])
+    thd = np.array([1.2, -0.4, 3.0])
+    out = kb.compute(th[:, None], thd[:, None])
+    torch.cuda.synchronize()
+    for e in range(3):
+        Mk, Ck, Jp, bp = pendulum_known_answer(th[e], thd[e])
+        assert abs(out.M[e, 0, 0].item() - Mk) <= 1e-14 * Mk
+        assert abs(out.C[e, 0].item() - Ck) <= 1e-13
+        np.testing.assert_allclose(out.J[e, :3, 0].cpu().numpy(), Jp, atol=1e-15)
+        np.testing.assert_allclose(out.b[e, :3].cpu().numpy(), bp, atol=1e-13)
+    kb = KinematicsBatch(tree=free_body())
+    rng = np.random.default_rng(3)
+    q = rng.normal(size=(5, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    qpos = np.hstack([rng.normal(size=(5, 3)), q])
+    qvel = rng.normal(size=(5, 6))
+    out = kb.compute(qpos, qvel)
+    torch.cuda.synchronize()
+    for e in range(5):
+        Mk, Ck = free_body_known_answer(q[e], qvel[e, :3], qvel[e, 3:])
+        np.testing.assert_allclose(out.M[e].cpu().numpy(), Mk, atol=1e-14)
+        np.testing.assert_allclose(out.C[e].cpu().numpy(), Ck, atol=1e-13)

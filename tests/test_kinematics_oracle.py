@@ -15,7 +15,7 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "oracle"))
 import kinematics as kin  # noqa: E402
-from kin_trees import chain_tree, random_tree  # noqa: E402
+from kin_trees import chain_tree, free_body, pendulum, random_tree  # noqa: E402
 
 ROBOTS = ["unitree_go2", "walter_sr", "random_free", "random_fixed", "chain"]
 EPS = 1e-6
@@ -120,3 +120,57 @@ def test_bias_gravity_and_energy_balance(robot):
         lhs = v @ (C - g)
         rhs = 0.5 * v @ ((Mp - Mm) / (2 * EPS)) @ v
         assert abs(lhs - rhs) <= 1e-6 * (1 + abs(lhs))
+
+
+def pendulum_known_answer(th, thd, mass=1.5, length=0.7, izz=1e-3, armature=0.05, g=9.81):
+    """Closed forms (MuJoCo conventions): hinge about +y, bob at -L z rotated by th about y:
+    p = (-L sin th, 0, -L cos th).  M = m L^2 + I + armature; qfrc_bias = m g L sin th (gravity
+    only, no velocity terms for one dof); Jp = dp/dth; Jpdot thd = d^2p/dt^2 at thdd = 0."""
+    L = length
+    M = mass * L * L + izz + armature
+    C = mass * g * L * np.sin(th)
+    Jp = np.array([-L * np.cos(th), 0.0, L * np.sin(th)])
+    bp = np.array([L * np.sin(th), 0.0, L * np.cos(th)]) * thd * thd
+    return M, C, Jp, bp
+
+
+def test_pendulum_known_answer():
+    m = kin.KinModel(pendulum())
+    for th, thd in ((0.3, 1.2), (-1.1, -0.4), (2.5, 3.0)):
+        M, C, J, b = kin.kinematics(m, np.array([th]), np.array([thd]))
+        Mk, Ck, Jp, bp = pendulum_known_answer(th, thd)
+        np.testing.assert_allclose(M[0, 0], Mk, rtol=1e-14)
+        np.testing.assert_allclose(C[0], Ck, rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(J[:3, 0], Jp, atol=1e-15)
+        np.testing.assert_allclose(J[3:, 0], [0.0, 1.0, 0.0], atol=1e-15)   # Jr = hinge axis
+        np.testing.assert_allclose(b[:3], bp, atol=1e-13)
+        np.testing.assert_allclose(b[3:], 0.0, atol=1e-15)
+
+
+def free_body_known_answer(quat, v, w_body, mass=2.0, diag=(0.1, 0.2, 0.3), g=9.81):
+    """Free body, COM at the origin: MuJoCo's rotational dofs are body axes, so
+    M = blockdiag(m I3, I_body) and qfrc_bias = (m g e_z, w x (I_body w)) in those coordinates."""
+    Ib = np.diag(diag)
+    M = np.zeros((6, 6))
+    M[:3, :3] = mass * np.eye(3)
+    M[3:, 3:] = Ib
+    C = np.concatenate([[0.0, 0.0, mass * g], np.cross(w_body, Ib @ w_body)])
+    return M, C
+
+
+def test_free_body_known_answer():
+    m = kin.KinModel(free_body())
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        v, w = rng.normal(size=3), rng.normal(size=3)
+        qpos = np.concatenate([rng.normal(size=3), q])
+        M, C, J, b = kin.kinematics(m, qpos, np.concatenate([v, w]))
+        Mk, Ck = free_body_known_answer(q, v, w)
+        np.testing.assert_allclose(M, Mk, atol=1e-14)
+        np.testing.assert_allclose(C, Ck, atol=1e-13)
+        R = kin.quat2mat(q)
+        np.testing.assert_allclose(J[:3], np.hstack([np.eye(3), np.zeros((3, 3))]), atol=1e-15)
+        np.testing.assert_allclose(J[3:], np.hstack([np.zeros((3, 3)), R]), atol=1e-15)
+        np.testing.assert_allclose(b, 0.0, atol=1e-14)   # origin = COM: no bias acceleration
