@@ -181,7 +181,8 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
 
 
 def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
-    """SURVEY.md §8d warm runs: a 10-step 1 % random walk of all inputs (made on the device before
+    """SURVEY.md §8d warm runs: a 10-step 1 % random walk of the inputs (M by an SPD-preserving
+    congruence; made on the device before
     timing, replayed ping-pong so consecutive ticks always differ by one walk step), solved with
     the warm state carried from tick to tick (osc_batch_solve_warm; the reference's SetWarmStart,
     operational_space_controller.h:519-526).  Reported beside the cold headline, not as it."""
@@ -195,10 +196,14 @@ def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, st
             if i == 5:                                   # contact mask: unchanged
                 new.append(t)
                 continue
-            w = t * (1.0 + 0.01 * torch.randn(t.shape, generator=g, device=t.device,
-                                              dtype=t.dtype))
-            if i == 0:                                   # M: symmetric, kept SPD
-                w = 0.5 * (w + w.transpose(1, 2)) + 1e-3 * eye
+            if i == 0:   # M: congruence A M A' keeps it SPD (osc_amd.synth.random_walk)
+                A = eye + 0.01 / nv ** 0.5 * torch.randn(t.shape, generator=g, device=t.device,
+                                                         dtype=t.dtype)
+                w = A @ t @ A.transpose(1, 2)
+                w = 0.5 * (w + w.transpose(1, 2))
+            else:
+                w = t * (1.0 + 0.01 * torch.randn(t.shape, generator=g, device=t.device,
+                                                  dtype=t.dtype))
             new.append(w.contiguous())
         seq.append(tuple(new))
     order = list(range(10)) + list(range(8, 0, -1))

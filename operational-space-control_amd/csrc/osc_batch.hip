@@ -65,6 +65,8 @@ struct DevParams {
   double eps_mu;
   double inf_thresh;
   double warm_delta;                 // warm start: slacks / multipliers floored at this value
+  double warm_center;                // warm start: no pair s_i lambda_i below this x their mean
+  int32_t warm_restart;              // warm start: re-centre an env still far off at this iteration
   int32_t max_iter;
 };
 
@@ -835,11 +837,14 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   a1 = -x1;
 }
 
-template <class D, bool SMALL>
+// WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
+// is unchanged by it: the two-wave Go2 variant would otherwise spill more).
+template <class D, bool SMALL, bool WARM>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
-    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm) {
+    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
+    int fixup) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
   constexpr bool HRL = SMALL && hr_fits_lds<D>();
@@ -850,6 +855,14 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   const int env_raw = blockIdx.x * kEnvPerWave + grp;
   const bool valid = env_raw < nenv;
   const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
+  // Fix-up pass after a warm-started solve: only wavefronts holding an env that did not converge
+  // run (cold, from the same workspace); only those envs' outputs are rewritten.
+  bool write_out = valid;
+  if constexpr (WARM) {
+    const bool redo = valid && fixup && gstatus[env] != OSC_SOLVE_OK;
+    if (fixup && __ballot(redo) == 0) return;
+    write_out = valid && (!fixup || redo);
+  }
 
   double* B = sm + grp * LY::IL;
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
@@ -1139,18 +1152,21 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   // no registers to spare)
   // A contact-mode switch (mask differs from the state's) changes the QP's rows: start cold.
   bool warm = false;
-  if (gwarm != nullptr) {
+  if (WARM && !fixup) {
     const double* w0 = gwarm + static_cast<size_t>(env) * D::WW;
     const double same = (l >= NC || w0[D::WW_M + l] == sMask[l]) ? 1.0 : 0.0;
     warm = row_min(same) == 1.0 && w0[0] == 1.0 && m_act > 0.0;
   }
-  const bool any_warm = __ballot(warm) != 0;
-  const bool all_warm = __ballot(!warm) == 0;
+  bool any_warm = false, all_warm = false;
+  if constexpr (WARM) {
+    any_warm = __ballot(warm) != 0;
+    all_warm = __ballot(!warm) == 0;
+  }
   for (int it = all_warm ? 0 : -1;; ++it) {
     STAMP_BEGIN();
     const bool init = it < 0;
     double mu = 0.0;
-    if (it == 0 && any_warm) {
+    if (WARM && it == 0 && any_warm) {
       const double* wst = gwarm + static_cast<size_t>(env) * D::WW;
       if (warm) {
         y0 = wst[D::WW_Y + j0];
@@ -1171,13 +1187,54 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
           lam[t] = act[t] ? fmax(wl, dlt) : 0.0;
         }
       }
+      // centre the warm pairs: no s_i lambda_i below warm_center x their mean (numpy model, 1 %
+      // random walk, 0.1: WaLTER mean 9.2 -> 6.5 iterations, lockstep 11.3 -> 7.8; Go2 6.6 ->
+      // 5.8; most warm stalls vanish)
+      double c0s = 0.0;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) c0s += act[t] ? s[t] * lam[t] : 0.0;
+      const double mu0 = P->warm_center * row_sum(c0s) / fmax(m_act, 1.0);
+      if (warm) {
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          if (act[t]) {
+            lam[t] = fmax(lam[t], mu0 * recip(s[t]));
+            s[t] = fmax(s[t], mu0 * recip(lam[t]));
+          }
+        }
+      }
+    }
+    // A warm-started env still unconverged after warm_restart iterations is re-centred in place
+    // (slacks h - G y + 1, multipliers 1: the cold start's shape, no factorisation) -- the rare
+    // warm starts that jam near a degenerate contact then finish like a cold solve instead of
+    // running to max_iter (tools/warm_stalls.py).
+    // (only an env still far from converged, mu > 1e-6: a slow but converging one is left alone)
+    bool restart = false;
+    if (WARM && any_warm && it == P->warm_restart) {
+      double cr = 0.0;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) cr += act[t] ? s[t] * lam[t] : 0.0;
+      const bool far = row_sum(cr) / fmax(m_act, 1.0) > 1e-6;
+      restart = __ballot(warm && !done && far) != 0;
+      if (restart) {
+        uv_product(sVy);
+        wave_sync();
+      }
+      if (restart && warm && !done && far) {
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          const double slack = h[t] - Gv(sVy, t);
+          s[t] = act[t] ? fmax(slack, 0.0) + 1.0 : 1.0;
+          lam[t] = act[t] ? 1.0 : 0.0;
+        }
+      }
     }
     if (!init) {
       double cs = 0.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) cs += act[t] ? s[t] * lam[t] : 0.0;
       mu = row_sum(cs) / fmax(m_act, 1.0);
-      const bool fresh = it == 0 || mu <= 1e-6;
+      const bool fresh = it == 0 || mu <= 1e-6 || restart;
       if (__ballot(fresh) != 0) {   // wave-uniform: the product uses the whole row's lanes
         uv_product(sVy);
         wave_sync();
@@ -1380,7 +1437,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 #pragma unroll
     for (int i = 0; i < NY; ++i) tq = fma(sU[l * NY1P + i], sVy[i], tq);
     sTau[l] = tq;
-    if (valid) gtau[static_cast<size_t>(env) * NU + l] = tq;
+    if (write_out) gtau[static_cast<size_t>(env) * NU + l] = tq;
   }
   if (gx != nullptr && l < NB) {
     const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + l * NY1P;
@@ -1392,7 +1449,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   wave_sync();
   const double fin = (isfinite(y0) && (!v1 || isfinite(y1))) ? 1.0 : 0.0;
   if (row_min(fin) == 0.0) st = OSC_SOLVE_NUMERICAL;
-  if (valid) {
+  if (write_out) {
     if (gx != nullptr) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
@@ -1409,9 +1466,9 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     }
     if (l == 0) {
       if (gstatus) gstatus[env] = st;
-      if (giters) giters[env] = it_done;
+      if (giters) giters[env] = (WARM && fixup) ? P->max_iter + it_done : it_done;   // both passes
     }
-    if (gwarm != nullptr) {   // this tick's y and lambda for the next one (NaN: next tick cold)
+    if (WARM) {   // this tick's y and lambda for the next one (NaN: next tick cold)
       double* wo = gwarm + static_cast<size_t>(env) * D::WW;
       wo[D::WW_Y + j0] = y0;
       if (v1) wo[D::WW_Y + j1] = y1;
@@ -1503,7 +1560,14 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.eps_mu = d.eps_mu;
   hp.inf_thresh = thresh;
   hp.max_iter = d.max_iter;
-  hp.warm_delta = 0.1;   // tools/ipm_model.py warm-start study: 1 % random walk, Go2 mean 11.1 -> 7.4
+  // warm start: numpy-model studies on a 1 % random walk; the OSC_WARM_* variables
+  // exist for the diagnostic sweeps (tools/warm_stalls.py), not for production use
+  hp.warm_delta = 0.1;
+  hp.warm_center = 0.3;
+  hp.warm_restart = 16;
+  if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
+  if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);
+  if (const char* e = std::getenv("OSC_WARM_CENTER")) hp.warm_center = std::atof(e);
 
   osc_model* m = new (std::nothrow) osc_model;
   if (!m) return OSC_ERR_DEVICE;
@@ -1552,7 +1616,10 @@ extern "C" int osc_model_get_desc(const osc_model* model, osc_model_desc* desc) 
 
 extern "C" int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes) {
   if (!model || !bytes || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
-  *bytes = sizeof(double) * static_cast<size_t>(ws_doubles(model->kid)) * static_cast<size_t>(nenv);
+  // per-env reduced QPs, then int32 solve-status scratch for the warm fix-up pass (16-B padded)
+  const size_t n = static_cast<size_t>(nenv);
+  *bytes = sizeof(double) * static_cast<size_t>(ws_doubles(model->kid)) * n +
+           ((sizeof(int32_t) * n + 15) & ~static_cast<size_t>(15));
   return OSC_OK;
 }
 
@@ -1572,12 +1639,29 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one
     // wave per SIMD, Hr in LDS where it fits); otherwise the two-waves-per-SIMD variant.
     const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
-    if (nenv <= model->small_batch_max)
-      hipLaunchKernelGGL((osc_ipm_kernel<D, true>), dim3(nb), dim3(kWave), 0, s, model->dparams,
-                         nenv, mask, ws, tau, x, status, iters, warm);
-    else
-      hipLaunchKernelGGL((osc_ipm_kernel<D, false>), dim3(nb), dim3(kWave), 0, s, model->dparams,
-                         nenv, mask, ws, tau, x, status, iters, warm);
+    // A warm-started solve is followed by a cold fix-up pass over the wavefronts that hold an
+    // env the warm start did not bring to convergence (it needs the per-env status: the
+    // caller's array, else scratch at the end of the workspace).
+    if (warm != nullptr && status == nullptr)
+      status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
+    const bool small = nenv <= model->small_batch_max;
+    if (warm == nullptr) {
+      if (small)
+        hipLaunchKernelGGL((osc_ipm_kernel<D, true, false>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+      else
+        hipLaunchKernelGGL((osc_ipm_kernel<D, false, false>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+    } else {
+      for (int pass = 0; pass < 2; ++pass) {
+        if (small)
+          hipLaunchKernelGGL((osc_ipm_kernel<D, true, true>), dim3(nb), dim3(kWave), 0, s,
+                             model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
+        else
+          hipLaunchKernelGGL((osc_ipm_kernel<D, false, true>), dim3(nb), dim3(kWave), 0, s,
+                             model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
+      }
+    }
   }
 }
 

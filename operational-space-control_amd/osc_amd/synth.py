@@ -77,15 +77,21 @@ def generate(robot: str, nenv: int, seed: int, scenario: str = "standing",
 
 
 def random_walk(inputs: dict, rng: np.random.Generator, scale: float = 0.01) -> dict:
-    """One step of the 1 % multiplicative random walk used for warm-start runs."""
+    """One step of the 1 % random walk used for warm-start runs: C, J, b, T
+    entrywise multiplicative; M by a congruence M' = A M A' with A = I + scale E / sqrt(nv), E
+    standard normal, so M stays symmetric positive definite (an entrywise 1 % walk of M drifts
+    indefinite within a few dozen steps, its smallest eigenvalue being 1e-2 of the largest)."""
     out = {}
     for k, v in inputs.items():
         if k == "mask":
             out[k] = v.copy()
             continue
-        w = v * (1.0 + scale * rng.standard_normal(v.shape))
         if k == "M":
+            n = v.shape[-1]
+            A = np.eye(n) + scale / np.sqrt(n) * rng.standard_normal(v.shape)
+            w = np.einsum("eij,ejk,elk->eil", A, v, A)
             w = 0.5 * (w + np.transpose(w, (0, 2, 1)))
-            w += 1e-3 * np.eye(w.shape[-1])      # keep SPD under the perturbation
+        else:
+            w = v * (1.0 + scale * rng.standard_normal(v.shape))
         out[k] = w
     return out
