@@ -117,8 +117,9 @@ int osc_model_destroy(osc_model* model);
 /* Copy of the descriptor a model was created from. */
 int osc_model_get_desc(const osc_model* model, osc_model_desc* desc);
 
-/* Device scratch the solve needs for `nenv` environments (the per-env reduced QP handed from
- * the assembly kernel to the interior-point kernel): 8.5 KB (Go2) / 12.3 KB (WaLTER) per env. */
+/* Device scratch the solve needs for `nenv` environments: the per-env reduced QP handed from
+ * the assembly kernel to the interior-point kernel (8.5 KB Go2 / 12.3 KB WaLTER per env), then
+ * 4 B per env of solve-status scratch used by the warm-start fix-up pass. */
 int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
 
 /* Batched solve; see the header comment for layouts.  Device pointers, async on `stream`.
@@ -154,7 +155,9 @@ int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double
  * contact mask differs from the state's (a contact-mode switch changes the QP's rows), or when
  * it has no inequality rows.  Each call reads the state and writes this tick's solution back.
  * Results agree with the cold solve to the solve's tolerance; the iteration count drops when
- * consecutive ticks are close. */
+ * consecutive ticks are close.  A warm env that stalls is re-centred in place,
+ * and any env the warm pass leaves unconverged is re-solved cold by a second launch that only
+ * the wavefronts holding such an env execute. */
 int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
 int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
                          const double* M, const double* C, const double* J, const double* b,
