@@ -67,6 +67,7 @@ struct DevParams {
   double warm_delta;                 // warm start: slacks / multipliers floored at this value
   double warm_center;                // warm start: no pair s_i lambda_i below this x their mean
   int32_t warm_restart;              // warm start: re-centre an env still far off at this iteration
+  int32_t restart_iter;              // cold start: the same, later
   int32_t max_iter;
 };
 
@@ -1204,23 +1205,26 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
         }
       }
     }
-    // A warm-started env still unconverged after warm_restart iterations is re-centred in place
-    // (slacks h - G y + 1, multipliers 1: the cold start's shape, no factorisation) -- the rare
-    // warm starts that jam near a degenerate contact then finish like a cold solve instead of
-    // running to max_iter (tools/warm_stalls.py).
-    // (only an env still far from converged, mu > 1e-6: a slow but converging one is left alone)
+    // An env still far from converged (mu > 1e-6) at iteration `restart_iter` (warm-started:
+    // `warm_restart`) is re-centred in place -- slacks h - G y + 1, multipliers 1: the cold
+    // start's shape, no factorisation.  The rare solves that fall into a two-iteration limit
+    // cycle of the step rule (mu oscillating near 1e-4; random-walk inputs, ~3e-6 of env-ticks,
+    // tools/warm_stalls.py) then finish ~10 iterations later instead of at max_iter.  No env of
+    // the fresh-batch sweeps is still that far off at iteration 20 (tools/ipm_model.py
+    // "recenter20": identical iteration counts).
     bool restart = false;
-    if (WARM && any_warm && it == P->warm_restart) {
+    if (it == P->restart_iter || (WARM && any_warm && it == P->warm_restart)) {
       double cr = 0.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) cr += act[t] ? s[t] * lam[t] : 0.0;
       const bool far = row_sum(cr) / fmax(m_act, 1.0) > 1e-6;
-      restart = __ballot(warm && !done && far) != 0;
+      const bool mine = far && !done && it == (warm ? P->warm_restart : P->restart_iter);
+      restart = __ballot(mine) != 0;
       if (restart) {
         uv_product(sVy);
         wave_sync();
       }
-      if (restart && warm && !done && far) {
+      if (mine) {
 #pragma unroll
         for (int t = 0; t < NRL; ++t) {
           const double slack = h[t] - Gv(sVy, t);
@@ -1565,6 +1569,8 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.warm_delta = 0.1;
   hp.warm_center = 0.3;
   hp.warm_restart = 16;
+  hp.restart_iter = 28;
+  if (const char* e = std::getenv("OSC_RESTART_ITER")) hp.restart_iter = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);
   if (const char* e = std::getenv("OSC_WARM_CENTER")) hp.warm_center = std::atof(e);

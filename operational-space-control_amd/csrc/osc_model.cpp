@@ -215,7 +215,7 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   desc->z_ub[0] = inf;  desc->z_ub[1] = inf;  desc->z_ub[2] = big_number;
   desc->infinity = inf;
   desc->eps_mu = 1e-12;
-  desc->max_iter = 40;
+  desc->max_iter = 50;   // normal solves take <= 24; the margin covers a re-centred stall
   return OSC_OK;
 }
 

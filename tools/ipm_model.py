@@ -181,6 +181,11 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
     eta = 0.99
     rp_c = None
     for it in range(max_iter + 1):
+        for v in variant:
+            if v.startswith("recenter") and it == int(v[8:]) and s @ lam / m > 1e-6:
+                s = np.maximum(h - G @ y, 0.0) + 1.0   # re-centre a stalled iterate in place
+                lam = np.ones(m)
+                rp_c = None
         rp = G @ y + s - h
         thr = [float(v[7:]) for v in variant if v.startswith("rpcarry") and len(v) > 7]
         mu_now = s @ lam / m
@@ -295,6 +300,9 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
                 eta = max(0.99, 1.0 - mu, 1.0 - (1.0 - a_aff) * float(v[4:]))
             if v.startswith("cap"):         # eta <= 1 - c
                 eta = min(eta, 1.0 - float(v[3:]))
+            if v.startswith("etalate"):     # from iteration k on: eta = max(0.99, 1 - mu), capped
+                if it >= int(v[7:]):
+                    eta = min(max(0.99, 1.0 - mu), 1.0 - 1e-5)
         alpha = min(1.0, eta * a)
         if TRACE is not None:
             TRACE.append((it, mu, a_aff, a, alpha, sig, float(np.abs(rp).max()),

@@ -1,7 +1,8 @@
 """Diagnostic: warm-started ticks over the bench's 1 % random walk (bench.py warm_ticks); dumps
 every env that does not converge (inputs of that tick + the warm state it started from) to
 gpurun_out/warm_stalls_<robot>.npz.
-    python tools/warm_stalls.py [robot] [nenv] [cycles]"""
+    python tools/warm_stalls.py [robot] [nenv] [cycles] [scenario] [mask]
+mask "bernoulli" redraws a Bernoulli(0.75) contact mask every tick (contact-mode switching)."""
 import os
 import sys
 
@@ -18,8 +19,10 @@ from osc_amd.dist import shard_seed  # noqa: E402
 robot = sys.argv[1] if len(sys.argv) > 1 else "walter_sr"
 nenv = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 cycles = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+scenario = sys.argv[4] if len(sys.argv) > 4 else "standing"
+mask_mode = sys.argv[5] if len(sys.argv) > 5 else "ones"
 solver = OSCBatchSolver(robot)
-inputs = solver.prepare(**generate(robot, nenv, shard_seed(0), "standing", "ones"))
+inputs = solver.prepare(**generate(robot, nenv, shard_seed(0), scenario, mask_mode))
 g = torch.Generator(device=inputs[0].device).manual_seed(shard_seed(0) + 7)
 nv = inputs[0].shape[1]
 eye = torch.eye(nv, dtype=torch.float64, device=inputs[0].device)
@@ -47,11 +50,14 @@ dump = []
 for k in range(cycles * len(order)):
     before = warm.clone()
     args = seq[order[k % len(order)]]
+    if mask_mode == "bernoulli":
+        m = (torch.rand(args[5].shape, generator=g, device=args[5].device) < 0.75).double()
+        args = args[:5] + (m,)
     solver.solve_warm_into(out, warm, *args)
     st = out.status.cpu().numpy()
     bad = np.nonzero(st != 0)[0]
     its = out.iters.cpu().numpy()
-    fix = np.nonzero(its > 40)[0]     # re-solved cold by the fix-up pass (iters = 40 + cold)
+    fix = np.nonzero(its > solver.desc.max_iter)[0]   # re-solved by the fix-up pass (max_iter + cold)
     print(f"tick {k}: mean_it {its.mean():.2f} max_it {its.max()} bad {bad.tolist()} "
           f"fixed_up {fix.tolist()}", flush=True)
     per = before.numel() // nenv
