@@ -107,6 +107,28 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
 
     kin_ms = timed(lambda: kb.compute_into(kout, qpos, qvel))
     tick_ms = timed(lambda: kb.solve_into(solver, out, qpos, qvel, T, mask, ws))
+    # a control loop: 10 consecutive joint states (joint angles +-0.01 rad, velocities +-1 % per
+    # step, base quaternion re-normalised), replayed ping-pong, warm state carried tick to tick
+    g = torch.Generator(device=qpos.device).manual_seed(seed + 11)
+    states = [(qpos, qvel)]
+    for _ in range(9):
+        q, v = states[-1]
+        q = q + 0.01 * torch.randn(q.shape, generator=g, device=q.device, dtype=q.dtype)
+        q[:, 3:7] = q[:, 3:7] / q[:, 3:7].norm(dim=1, keepdim=True)
+        q[:, 0:3] = 0.0                                  # base position 0 (osc.h:358-359)
+        v = v * (1.0 + 0.01 * torch.randn(v.shape, generator=g, device=v.device, dtype=v.dtype))
+        states.append((q.contiguous(), v.contiguous()))
+    order = list(range(10)) + list(range(8, 0, -1))
+    warm = solver.alloc_warm_state(nenv)
+    k = [0]
+
+    def warm_tick():
+        q, v = states[order[k[0] % len(order)]]
+        kb.solve_warm_into(solver, out, warm, q, v, T, mask, ws)
+        k[0] += 1
+    for _ in range(len(order)):
+        warm_tick()
+    warm_ms = timed(warm_tick)
     nq, nv, ns = kb.nq, kb.nv, kb.ns
     kin_bytes = 8 * (nq + nv + nv * nv + nv + 6 * ns * nv + 6 * ns)
     gbs = kin_bytes * nenv / (kin_ms * 1e-3) / 1e9
@@ -115,7 +137,10 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "bytes_per_env": kin_bytes},
             "tick_from_joint_states_ms": tick_ms,
-            "tick_from_joint_states_solves_per_s": nenv / (tick_ms * 1e-3)}
+            "tick_from_joint_states_solves_per_s": nenv / (tick_ms * 1e-3),
+            "tick_from_joint_states_warm_ms": warm_ms,
+            "tick_from_joint_states_warm_solves_per_s": nenv / (warm_ms * 1e-3),
+            "tick_from_joint_states_warm_mean_ipm_iters": float(out.iters.double().mean().item())}
 
 
 def run_mixed(args, world, rank, dev, barrier) -> None:

@@ -1568,7 +1568,7 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   // exist for the diagnostic sweeps (tools/warm_stalls.py), not for production use
   hp.warm_delta = 0.1;
   hp.warm_center = 0.3;
-  hp.warm_restart = 16;
+  hp.warm_restart = 22;
   hp.restart_iter = 28;
   if (const char* e = std::getenv("OSC_RESTART_ITER")) hp.restart_iter = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
