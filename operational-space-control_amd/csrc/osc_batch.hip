@@ -1028,6 +1028,15 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const double v = (jc == 0) ? v0 : ((jc == 1) ? v1 : v2);
     return jk >= 0 ? v : 0.0;
   };
+  // this lane's two U columns, loop-invariant, kept in registers (AGPR spill space in SMALL)
+  double uc0[SMALL ? NU : 1], uc1[SMALL ? NU : 1];
+  if constexpr (SMALL) {
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      uc0[q] = sU[q * NY1P + j0];
+      uc1[q] = sU[q * NY1P + jj1];
+    }
+  }
   auto GTw2 = [&](const double* w, double& r0, double& r1) {
     double a0 = 0.0, a1 = 0.0;
     if constexpr (SMALL) {
@@ -1040,8 +1049,8 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       }
 #pragma unroll
       for (int q = 0; q < NU; ++q) {
-        u0[q] = sU[q * NY1P + j0];
-        u1[q] = sU[q * NY1P + jj1];
+        u0[q] = uc0[q];
+        u1[q] = uc1[q];
       }
       const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
 #pragma unroll
