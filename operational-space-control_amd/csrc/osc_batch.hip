@@ -944,22 +944,27 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   STAMP_END(0);
 
   // U_y v for the torque rows (lanes l < NU), result in sUv; caller syncs
+  // the torque lanes' own U rows (loop-invariant) in registers for the one-wave Go2 variant
+  constexpr bool kURowReg = SMALL && NY % 2 == 0 && NY <= 24;
+  double urow[kURowReg ? NY : 1];
+  if constexpr (kURowReg) {
+    const int lr = l < NU ? l : 0;
+#pragma unroll
+    for (int i = 0; i < NY; ++i) urow[i] = sU[lr * NY1P + i];
+  }
   auto uv_product = [&](const double* v) {
     if (l < NU) {
       double a = 0.0;
-      // 16-byte reads, all issued before the FMAs.  Measured per system (tools/eps_sweep.py):
+      // reads of v issued before the FMAs.  Measured per system (tools/eps_sweep.py):
       // Go2 (24 columns) 0.268 -> 0.261 ms; WaLTER (32) slower, its registers are the limit.
-      if constexpr (SMALL && NY % 2 == 0 && NY <= 24) {
-        double2 u[NY / 2], x[NY / 2];
+      if constexpr (kURowReg) {
+        double2 x[NY / 2];
+#pragma unroll
+        for (int i = 0; i < NY / 2; ++i) x[i] = *reinterpret_cast<const double2*>(v + 2 * i);
 #pragma unroll
         for (int i = 0; i < NY / 2; ++i) {
-          u[i] = *reinterpret_cast<const double2*>(sU + l * NY1P + 2 * i);
-          x[i] = *reinterpret_cast<const double2*>(v + 2 * i);
-        }
-#pragma unroll
-        for (int i = 0; i < NY / 2; ++i) {
-          a = fma(u[i].x, x[i].x, a);
-          a = fma(u[i].y, x[i].y, a);
+          a = fma(urow[2 * i], x[i].x, a);
+          a = fma(urow[2 * i + 1], x[i].y, a);
         }
       } else {
 #pragma unroll
