@@ -133,12 +133,14 @@ int osc_batch_solve(const osc_model* model, int32_t nenv,
 
 /* The two halves of osc_batch_solve, for callers that time, overlap or reuse them.
  * osc_batch_assemble builds every environment's reduced QP (the six CasADi evaluations +
- * OSQP stacking of operational_space_controller.h:457-529, condensed onto y = (dv_a, z)) into
- * `workspace`; osc_batch_solve_assembled runs the interior-point solve on it and writes the
- * outputs exactly as osc_batch_solve does (contact_mask must be the one assembled with).
- * Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its layout per
+ * OSQP stacking of operational_space_controller.h:457-529, condensed onto NY = nu + 3nc reduced
+ * variables y) into `workspace`; osc_batch_solve_assembled runs the interior-point solve on it
+ * and writes the outputs exactly as osc_batch_solve does (contact_mask must be the one assembled
+ * with).  Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its layout per
  * environment, in doubles: [g (NY, padded even) | U (NU x (NY+1) padded) | Hr (NY x NY) |
- * X (NB x (NY+1) padded)], NY = nu + 3nc, NB = nv - nu; stride osc_workspace_bytes / nenv. */
+ * X (NX x (NY+1) padded)]; stride osc_workspace_bytes / nenv.  Two coordinate systems
+ * (DESIGN.md §3): y = (dv_a, z) with dv_b = X [y;1], NX = nv - nu, u = U [y;1] (walter_sr), or
+ * y = (u, z) with dv = X [y;1], NX = nv, U = [I | 0] (unitree_go2). */
 int osc_batch_assemble(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask,

@@ -74,12 +74,17 @@ struct DevParams {
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regions 16-B aligned
 
-template <int NV_, int NU_, int NC_, int NS_>
+// TY_ selects the reduced coordinates: false -> y = (dv_a, z), u = U [y; 1] (dense torque rows,
+// only the base block M_bb is inverted); true -> y = (u, z), dv = X [y; 1] = M^-1 (B u + Jc z - C)
+// over all nv rows, so the torque bounds are plain bounds on y (diagonal in the Newton matrix).
+template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
+  static constexpr bool TY = TY_;
   static constexpr int NB = NV - NU;          // unactuated (floating-base) dofs
+  static constexpr int NXR = TY ? NV : NB;    // rows of X: the dv entries that are not in y
   static constexpr int NZ = 3 * NC;
-  static constexpr int NY = NU + NZ;          // reduced variables (dv_a, z)
+  static constexpr int NY = NU + NZ;          // reduced variables (dv_a or u, z)
   static constexpr int NY1 = NY + 1;          // + affine column
   static constexpr int NY1P = even(NY1);      // padded row stride of U and X
   static constexpr int S = 6 * NS;            // task rows
@@ -99,7 +104,7 @@ struct Dims {
   static constexpr int W_U = even(NY);
   static constexpr int W_HR = W_U + NU * NY1P;
   static constexpr int W_X = W_HR + even(NY * NY);
-  static constexpr int WS = W_X + NB * NY1P;
+  static constexpr int WS = W_X + NXR * NY1P;
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
   static constexpr int WW_Y = 2;
   static constexpr int WW_L = WW_Y + even(NY);
@@ -123,9 +128,10 @@ struct Dims {
   static constexpr int O_M = R1, O_C = R1 + even(NV * NV), O_G = R1;
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
-  static constexpr int O_U = O_X + NB * NY1P;
+  static constexpr int O_U = O_X + NXR * NY1P;
   static constexpr int O_MASK = O_U + NU * NY1P;
-  static constexpr int SMEM = O_MASK + even(NC);
+  static constexpr int O_DM = O_MASK + even(NC);         // TY: 1/D of M = L D L'
+  static constexpr int SMEM = O_DM + (TY ? even(NV) : 0);
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
@@ -151,7 +157,7 @@ struct IpmLayout {
   static constexpr int I_MASK = I_DR + D::NRL * kRow;
   static constexpr int I_TAU = I_MASK + even(NC);
   static constexpr int I_XB = I_TAU + even(NU);
-  static constexpr int I_DINV = I_XB + even(NB);          // 1/D of the factorization (32)
+  static constexpr int I_DINV = I_XB + even(D::NXR);      // 1/D of the factorization (32)
   static constexpr int IL = I_DINV + 2 * kRow;
 };
 template <class D>
@@ -396,7 +402,7 @@ __device__ __forceinline__ void upper_pair(int p, int& i, int& j) {
 
 // ============================ kernel 1: reduced QP per env ==================================
 template <class D>
-__global__ __launch_bounds__(kWave) void osc_setup_kernel(
+__global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
@@ -495,6 +501,79 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   // and the torque map U = M_a Pm + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
   // (dynamics rows: autogen.py:58-89; Jc = Jp[last 3nc rows]^T: osc.h:439-445)
   constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
+  if constexpr (D::TY) {
+    // y = (u, z):  X = M^-1 [B | Jc | -C]  over all NV rows, U = [I_nu | 0].
+    // L D L' of the whole M in place (lower triangle of sM), right-looking with the unscaled
+    // pivot column; each lane owns up to ceil(NV(NV+1)/2 / 64) entries of the lower triangle.
+    double* sDm = sm + D::O_DM;
+    constexpr int NPM = NV * (NV + 1) / 2;
+    constexpr int TM = (NPM + kWave - 1) / kWave;
+    int prow[TM], pcol[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int p = lane + t * kWave;
+      int a = 0, b = 0;
+      upper_pair<NV>(p < NPM ? p : NPM - 1, a, b);
+      prow[t] = b;
+      pcol[t] = p < NPM ? a : NV;   // NV: no entry
+    }
+#pragma unroll 1
+    for (int k = 0; k < NV; ++k) {
+      const double dk = recip1(sM[k * NV + k]);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        if (pcol[t] > k && pcol[t] < NV) {
+          const int i = prow[t], j = pcol[t];
+          sM[i * NV + j] = fma(-sM[i * NV + k] * dk, sM[j * NV + k], sM[i * NV + j]);
+        }
+      }
+      if (lane == 0) sDm[k] = dk;
+      wave_sync();
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)   // scale the strictly lower part to unit-lower L
+      if (pcol[t] < prow[t]) sM[prow[t] * NV + pcol[t]] *= sDm[pcol[t]];
+    wave_sync();
+    const int c = lane;
+    if (c < NY1) {
+      // right-hand side column c of [B | Jc | -C] (pinned contact columns: 0)
+      const bool pinned = (c >= NU && c < NY) && (sMask[(c - NU) / 3] == 0.0);
+      const bool cu = c < NU, cz = !cu && c < NY;
+      const double* xp = cz ? sA + (JC0 + c - NU) * NAP : sC;
+      const double xsg = cz ? 1.0 : -1.0;
+      double x[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const double v = xsg * xp[i];
+        x[i] = cu ? ((i == NB + c) ? 1.0 : 0.0) : (pinned ? 0.0 : v);
+      }
+      // (a compiler fence every few steps keeps the L reads from all being hoisted at once)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+#pragma unroll
+        for (int i = k + 1; i < NV; ++i) x[i] = fma(-sM[i * NV + k], x[k], x[i]);
+        if (k % 3 == 2) asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) x[k] *= sDm[k];
+#pragma unroll
+      for (int k = NV - 1; k >= 0; --k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) x[i] = fma(-sM[k * NV + i], x[k], x[i]);
+        if (k % 3 == 0) asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) sX[i * NY1P + c] = x[i];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) sU[a * NY1P + c] = (a == c) ? 1.0 : 0.0;
+    } else if (c < NY1P) {   // padding column: read by the 2x2 tiles, must be 0
+#pragma unroll
+      for (int i = 0; i < NV; ++i) sX[i * NY1P + c] = 0.0;
+#pragma unroll
+      for (int a = 0; a < NU; ++a) sU[a * NY1P + c] = 0.0;
+    }
+    wave_sync();
+  } else {
   // One lane per column c of [y; 1]; when two copies of the 32-lane column set fit the wave,
   // both halves solve for X (redundantly) and split the NU rows of U between them.
   constexpr bool kSplitU = 2 * NY1P <= kWave;
@@ -569,7 +648,9 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
     for (int t = 0; t < kUStep; ++t)
       if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = 0.0;
   }
-  wave_sync();   // J, M, C dead from here on (R1, R2 get reused)
+  wave_sync();
+  }   // TY
+  // J, M, C dead from here on (R1, R2 get reused)
 
   STAMP_END(2);
   STAMP_BEGIN();
@@ -577,16 +658,22 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   // dv = Pm [y;1] with Pm = [X ; (I_nu 0 0)],  T1 = H_dv Pm (+ f_dv in the affine column),
   // Hr = Pm' T1 + 2 (w_tau + w_reg) U'U + 2 w_reg I_z,   g = last column.
   // T1 = H_dv Pm: one 2x2 tile (rows r0, r0+1 x columns c0, c0+1) per lane and round.
+  // (TY: Pm = X, no identity rows; the affine column still carries f_dv)
   auto t1_base = [&](int r, int c) -> double {
-    const double v = sHa[r * NA + ((c < NU) ? NB + c : NV)];   // read unconditionally
-    return (c < NU || c == NY) ? v : 0.0;
+    if constexpr (D::TY) {
+      const double v = sHa[r * NA + NV];
+      return c == NY ? v : 0.0;
+    } else {
+      const double v = sHa[r * NA + ((c < NU) ? NB + c : NV)];   // read unconditionally
+      return (c < NU || c == NY) ? v : 0.0;
+    }
   };
   for (int p = lane; p < D::NBT; p += kWave) {
     const int r0 = 2 * (p / D::NY2), c0 = 2 * (p % D::NY2);
     double t00 = t1_base(r0, c0), t01 = t1_base(r0, c0 + 1);
     double t10 = t1_base(r0 + 1, c0), t11 = t1_base(r0 + 1, c0 + 1);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
+#pragma unroll 6
+    for (int i = 0; i < D::NXR; ++i) {
       const double h0 = sHa[r0 * NA + i], h1 = sHa[(r0 + 1) * NA + i];
       const double2 x = *reinterpret_cast<const double2*>(sX + i * NY1P + c0);
       t00 = fma(h0, x.x, t00);
@@ -611,6 +698,7 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
       const double mk = sMask[kz < NC ? kz : NC - 1];      // read before any branch
       if (b >= NY1 || (a == NY && b == NY)) return;
       if (b < NY) {
+        if (D::TY && a == b && a < NU) acc += wu2;   // TY: U'U = I_nu
         if (a == b && a >= NU) {
           acc += wr2;
           if (mk == 0.0) acc = 1.0;   // pinned z: identity row
@@ -632,11 +720,11 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const double t1 = sT1[(NB + ((a0 + i < NU) ? a0 + i : NU - 1)) * NY1P + b0 + j];
-          h[i][j] = (a0 + i < NU) ? t1 : 0.0;
+          h[i][j] = (!D::TY && a0 + i < NU) ? t1 : 0.0;
           uu[i][j] = 0.0;
         }
-#pragma unroll
-      for (int r = 0; r < NB; ++r) {
+#pragma unroll 6
+      for (int r = 0; r < D::NXR; ++r) {
         const double2 xa = *reinterpret_cast<const double2*>(sX + r * NY1P + a0);
         const double2 tb = *reinterpret_cast<const double2*>(sT1 + r * NY1P + b0);
         h[0][0] = fma(xa.x, tb.x, h[0][0]);
@@ -645,7 +733,7 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
         h[1][1] = fma(xa.y, tb.y, h[1][1]);
       }
 #pragma unroll
-      for (int q = 0; q < NU; ++q) {
+      for (int q = 0; q < (D::TY ? 0 : NU); ++q) {
         const double2 ua = *reinterpret_cast<const double2*>(sU + q * NY1P + a0);
         const double2 ub = *reinterpret_cast<const double2*>(sU + q * NY1P + b0);
         uu[0][0] = fma(ua.x, ub.x, uu[0][0]);
@@ -668,7 +756,7 @@ __global__ __launch_bounds__(kWave) void osc_setup_kernel(
   for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
   for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
   for (int i = lane; i < NU * NY1P; i += kWave) w[D::W_U + i] = sU[i];
-  for (int i = lane; i < NB * NY1P; i += kWave) w[D::W_X + i] = sX[i];
+  for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
   STAMP_END(5);
   STAMP_STORE_SETUP();
 }
@@ -913,7 +1001,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       const double sg = (r & 1) ? -1.0 : 1.0;
       const double bnd = (r & 1) ? P->u_lb[q] : P->u_ub[q];
       act[t] = fabs(bnd) < P->inf_thresh;
-      h[t] = sg * (bnd - sU[q * NY1P + NY]);
+      h[t] = D::TY ? sg * bnd : sg * (bnd - sU[q * NY1P + NY]);   // TY: the row is +-y_q
     } else if (r < MI) {
       const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
       const double m = sMask[k];
@@ -945,15 +1033,16 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 
   // U_y v for the torque rows (lanes l < NU), result in sUv; caller syncs
   // the torque lanes' own U rows (loop-invariant) in registers for the one-wave Go2 variant
-  constexpr bool kURowReg = SMALL && NY % 2 == 0 && NY <= 24;
+  constexpr bool kURowReg = SMALL && !D::TY && NY % 2 == 0 && NY <= 24;
   double urow[kURowReg ? NY : 1];
   if constexpr (kURowReg) {
     const int lr = l < NU ? l : 0;
 #pragma unroll
     for (int i = 0; i < NY; ++i) urow[i] = sU[lr * NY1P + i];
   }
+  // (TY: the torque rows read y_q itself, there is no product)
   auto uv_product = [&](const double* v) {
-    if (l < NU) {
+    if (!D::TY && l < NU) {
       double a = 0.0;
       // reads of v issued before the FMAs.  Measured per system (tools/eps_sweep.py):
       // Go2 (24 columns) 0.268 -> 0.261 ms; WaLTER (32) slower, its registers are the limit.
@@ -982,7 +1071,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       const int r = l + kRow * t;
       const int q = (r < 2 * NU) ? (r >> 1) : 0;
       const int k = (r >= 2 * NU && r < MI) ? (r - 2 * NU) / 6 : 0;
-      uq[t] = sUv[q];
+      uq[t] = D::TY ? v[q] : sUv[q];
       f0[t] = v[NU + 3 * k];
       f1[t] = v[NU + 3 * k + 1];
       f2[t] = v[NU + 3 * k + 2];
@@ -1002,7 +1091,10 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   auto Gv = [&](const double* v, int t) -> double {
     if (!act[t]) return 0.0;
     const int r = l + kRow * t;
-    if (r < 2 * NU) return (r & 1) ? -sUv[r >> 1] : sUv[r >> 1];
+    if (r < 2 * NU) {
+      const double uq = D::TY ? v[r >> 1] : sUv[r >> 1];
+      return (r & 1) ? -uq : uq;
+    }
     const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
     const int z0 = NU + 3 * k;
     if (rt < 4) {
@@ -1034,8 +1126,9 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     return jk >= 0 ? v : 0.0;
   };
   // this lane's two U columns, loop-invariant, kept in registers (AGPR spill space in SMALL)
-  double uc0[SMALL ? NU : 1], uc1[SMALL ? NU : 1];
-  if constexpr (SMALL) {
+  constexpr bool kUCReg = SMALL && !D::TY;
+  double uc0[kUCReg ? NU : 1], uc1[kUCReg ? NU : 1];
+  if constexpr (kUCReg) {
 #pragma unroll
     for (int q = 0; q < NU; ++q) {
       uc0[q] = sU[q * NY1P + j0];
@@ -1044,7 +1137,16 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   }
   auto GTw2 = [&](const double* w, double& r0, double& r1) {
     double a0 = 0.0, a1 = 0.0;
-    if constexpr (SMALL) {
+    if constexpr (D::TY) {
+      // torque rows +-e_q: lane j0 < NU picks up w[2 j0] - w[2 j0 + 1]; slot j1 >= 16 > NU is
+      // a contact variable
+      const double2 p = *reinterpret_cast<const double2*>(w + 2 * (j0 < NU ? j0 : 0));
+      const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
+      r0 = (j0 < NU ? p.x - p.y : 0.0) + k0;
+      r1 = k1;
+      (void)a0;
+      (void)a1;
+    } else if constexpr (SMALL) {
       // one wave per SIMD: latency is exposed, registers are not short (AGPR spill space)
       double d[NU], u0[NU], u1[NU];
 #pragma unroll
@@ -1298,6 +1400,17 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     // rolled (I-cache, registers); the next row's three LDS reads are issued one trip ahead
     // (the sum of the two row weights is formed at use, not at load: adding at load time would
     // wait for the prefetch at the top of every trip)
+    if constexpr (D::TY) {
+      // TY: G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
+      static_assert(D::NU <= kRow, "TY: torque variables in the first column slot");
+      const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
+      const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
+      dg0 += du;
+      static_for<0, NU>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        c0[i] += keep_lanes<rows_mask(1u << i)>(du);
+      });
+    } else {
     double2 dd_n = *reinterpret_cast<const double2*>(sDr);
     double u0_n = sU[j0], u1_n = sU[jj1];
 #pragma unroll 1
@@ -1311,6 +1424,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
       dg0 = fma(t0, u0, dg0);
       dg1 = fma(t1, u1, dg1);
       rank1_rows<NY>(c0, c1, u0, u1, t0, t1);
+    }
     }
     STAMP_END(9);
     STAMP_BEGIN();
@@ -1451,18 +1565,24 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 
   // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
   if (l < NU) {
-    double tq = sU[l * NY1P + NY];
+    double tq = D::TY ? sVy[l] : sU[l * NY1P + NY];
 #pragma unroll
-    for (int i = 0; i < NY; ++i) tq = fma(sU[l * NY1P + i], sVy[i], tq);
+    for (int i = 0; i < (D::TY ? 0 : NY); ++i) tq = fma(sU[l * NY1P + i], sVy[i], tq);
     sTau[l] = tq;
     if (write_out) gtau[static_cast<size_t>(env) * NU + l] = tq;
   }
-  if (gx != nullptr && l < NB) {
-    const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + l * NY1P;
-    double xb = xr[NY];
+  if (gx != nullptr) {   // dv rows not in y: X [y; 1]  (TY: all NV of them, two per lane)
 #pragma unroll
-    for (int i = 0; i < NY; ++i) xb = fma(xr[i], sVy[i], xb);
-    sXb[l] = xb;
+    for (int t = 0; t < (D::NXR + kRow - 1) / kRow; ++t) {
+      const int rr = l + kRow * t;
+      if (rr < D::NXR) {
+        const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + rr * NY1P;
+        double xb = xr[NY];
+#pragma unroll
+        for (int i = 0; i < NY; ++i) xb = fma(xr[i], sVy[i], xb);
+        sXb[rr] = xb;
+      }
+    }
   }
   wave_sync();
   const double fin = (isfinite(y0) && (!v1 || isfinite(y1))) ? 1.0 : 0.0;
@@ -1474,7 +1594,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
         const int idx = l + kRow * t;
         if (idx < D::NX) {
           double v;
-          if (idx < NB) v = sXb[idx];
+          if (idx < D::NXR) v = sXb[idx];
           else if (idx < NV) v = sVy[idx - NB];
           else if (idx < NV + NU) v = sTau[idx - NV];
           else v = sVy[NU + idx - NV - NU];
@@ -1498,7 +1618,7 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   }
 }
 
-using Go2 = Dims<18, 12, 4, 5>;       // unitree_go2: nv 18, nu 12, 4 feet, 5 sites
+using Go2 = Dims<18, 12, 4, 5, true>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites; y = (u, z)
 using Walter = Dims<14, 8, 8, 17>;    // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
 
 enum KernelId { K_NONE = 0, K_GO2 = 1, K_WALTER = 2 };

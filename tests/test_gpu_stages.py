@@ -1,8 +1,10 @@
 """GPU stage parity: the reduced QP osc_batch_assemble builds (setup kernel, phases A-D) is checked against the
 oracle's full QP (oracle/osc_qp.py) through properties that do not depend on how the
 reduction is computed:
-  * x(y) = (dv_b = X[y;1], dv_a = y_u, u = U[y;1], z = y_z) satisfies the dynamics equality
-    M dv + C - B u - Jc z = 0 for ANY y    (autogen.py:87; checks X and U)
+  * x(y) satisfies the dynamics equality M dv + C - B u - Jc z = 0 for ANY y (autogen.py:87;
+    checks X and U), in either reduced coordinate system the kernel uses:
+      y = (dv_a, z): dv_b = X[y;1] (nb rows of X), dv_a = y_u, u = U[y;1]      (walter_sr)
+      y = (u, z):    dv = X[y;1] (nv rows of X), u = U[y;1] = y_u, U = [I | 0]  (unitree_go2)
   * 1/2 y'Hr y + g'y differs from the full objective 1/2 x'Hx + f'x by a constant
     (checks Hr and g against H, f of autogen.py:304-319)
 """
@@ -42,7 +44,8 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     o_g, o_u = 0, ev(ny)
     o_hr = o_u + nu * ny1p
     o_x = o_hr + ev(ny * ny)
-    assert sz == o_x + nb * ny1p                # layout documented in include/osc_batch.h
+    nxr = (sz - o_x) // ny1p                     # layout documented in include/osc_batch.h
+    assert nxr in (nb, nv) and sz == o_x + nxr * ny1p
     dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     rc = L.osc_batch_assemble(s._h, nenv, *[p(a) for a in args], p(dbg), nbytes,
@@ -56,7 +59,9 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
         Hr = D[e, o_hr:o_hr + ny * ny].reshape(ny, ny)
         g = D[e, o_g:o_g + ny]
         U = D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
-        X = D[e, o_x:].reshape(nb, ny1p)[:, :ny + 1]
+        X = D[e, o_x:].reshape(nxr, ny1p)[:, :ny + 1]
+        if nxr == nv:                           # torque coordinates: U = [I_nu | 0]
+            np.testing.assert_array_equal(U, np.eye(nu, ny + 1))
         np.testing.assert_array_equal(Hr, Hr.T)
         a = [inp[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a)
@@ -65,7 +70,7 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
 
         def x_of(y):
             y1 = np.append(y, 1.0)
-            dv = np.concatenate([X @ y1, y[:nu]])
+            dv = X @ y1 if nxr == nv else np.concatenate([X @ y1, y[:nu]])
             return np.concatenate([dv, U @ y1, y[nu:]])
 
         objs = []
