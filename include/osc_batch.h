@@ -140,7 +140,7 @@ int osc_batch_solve(const osc_model* model, int32_t nenv,
  * environment, in doubles: [g (NY, padded even) | U (NU x (NY+1) padded) | Hr (NY x NY) |
  * X (NX x (NY+1) padded)]; stride osc_workspace_bytes / nenv.  Two coordinate systems
  * (DESIGN.md §3): y = (dv_a, z) with dv_b = X [y;1], NX = nv - nu, u = U [y;1] (walter_sr), or
- * y = (u, z) with dv = X [y;1], NX = nv, U = [I | 0] (unitree_go2). */
+ * y = (u, z) with dv = X [y;1], NX = nv and no U block (u = y_u; unitree_go2). */
 int osc_batch_assemble(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask,

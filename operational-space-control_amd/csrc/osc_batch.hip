@@ -23,7 +23,7 @@
 //      G = [+-U (torque bounds, dense rows); pyramid + fz bound rows (sparse)].  Newton matrix
 //      K = Hr + G' diag(lambda/s) G, LDL^T with "Cholesky-infinity" pivots.
 //
-// Two kernels, one workspace (per env [Hr | g | U | X], fp64):
+// Two kernels, one workspace (per env [g | U | Hr | X], fp64; no U in torque coordinates):
 //   osc_setup_kernel  one 64-lane wavefront per environment.  Inputs are staged HBM -> LDS
 //                     with 16-byte loads; the dense products (J'WJ, the reduced Hessian) give
 //                     every lane several output entries.
@@ -101,8 +101,9 @@ struct Dims {
 
   // ---- workspace per env (doubles): [g | U | Hr | X] ----
   static constexpr int W_G = 0;
+  static constexpr int NUW = TY ? 0 : NU;     // rows of U kept (TY: U = [I | 0] is implicit)
   static constexpr int W_U = even(NY);
-  static constexpr int W_HR = W_U + NU * NY1P;
+  static constexpr int W_HR = W_U + NUW * NY1P;
   static constexpr int W_X = W_HR + even(NY * NY);
   static constexpr int WS = W_X + NXR * NY1P;
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
@@ -129,9 +130,8 @@ struct Dims {
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
   static constexpr int O_U = O_X + NXR * NY1P;
-  static constexpr int O_MASK = O_U + NU * NY1P;
-  static constexpr int O_DM = O_MASK + even(NC);         // TY: 1/D of M = L D L'
-  static constexpr int SMEM = O_DM + (TY ? even(NV) : 0);
+  static constexpr int O_MASK = O_U + NUW * NY1P;
+  static constexpr int SMEM = O_MASK + even(NC);
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
   double* sC = sm + D::O_C;
   double* sHa = sm + D::O_HA;
   double* sX = sm + D::O_X;
-  double* sU = sm + D::O_U;
+  double* sU = D::TY ? sm + D::O_X + NB * NY1P : sm + D::O_U;   // TY: U parked in X's last rows
   double* sMask = sm + D::O_MASK;
   double* sT1 = sm + D::O_T1;
   double* sHr = sm + D::O_HR;
@@ -501,79 +501,6 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
   // and the torque map U = M_a Pm + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
   // (dynamics rows: autogen.py:58-89; Jc = Jp[last 3nc rows]^T: osc.h:439-445)
   constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
-  if constexpr (D::TY) {
-    // y = (u, z):  X = M^-1 [B | Jc | -C]  over all NV rows, U = [I_nu | 0].
-    // L D L' of the whole M in place (lower triangle of sM), right-looking with the unscaled
-    // pivot column; each lane owns up to ceil(NV(NV+1)/2 / 64) entries of the lower triangle.
-    double* sDm = sm + D::O_DM;
-    constexpr int NPM = NV * (NV + 1) / 2;
-    constexpr int TM = (NPM + kWave - 1) / kWave;
-    int prow[TM], pcol[TM];
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      const int p = lane + t * kWave;
-      int a = 0, b = 0;
-      upper_pair<NV>(p < NPM ? p : NPM - 1, a, b);
-      prow[t] = b;
-      pcol[t] = p < NPM ? a : NV;   // NV: no entry
-    }
-#pragma unroll 1
-    for (int k = 0; k < NV; ++k) {
-      const double dk = recip1(sM[k * NV + k]);
-#pragma unroll
-      for (int t = 0; t < TM; ++t) {
-        if (pcol[t] > k && pcol[t] < NV) {
-          const int i = prow[t], j = pcol[t];
-          sM[i * NV + j] = fma(-sM[i * NV + k] * dk, sM[j * NV + k], sM[i * NV + j]);
-        }
-      }
-      if (lane == 0) sDm[k] = dk;
-      wave_sync();
-    }
-#pragma unroll
-    for (int t = 0; t < TM; ++t)   // scale the strictly lower part to unit-lower L
-      if (pcol[t] < prow[t]) sM[prow[t] * NV + pcol[t]] *= sDm[pcol[t]];
-    wave_sync();
-    const int c = lane;
-    if (c < NY1) {
-      // right-hand side column c of [B | Jc | -C] (pinned contact columns: 0)
-      const bool pinned = (c >= NU && c < NY) && (sMask[(c - NU) / 3] == 0.0);
-      const bool cu = c < NU, cz = !cu && c < NY;
-      const double* xp = cz ? sA + (JC0 + c - NU) * NAP : sC;
-      const double xsg = cz ? 1.0 : -1.0;
-      double x[NV];
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const double v = xsg * xp[i];
-        x[i] = cu ? ((i == NB + c) ? 1.0 : 0.0) : (pinned ? 0.0 : v);
-      }
-      // (a compiler fence every few steps keeps the L reads from all being hoisted at once)
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-#pragma unroll
-        for (int i = k + 1; i < NV; ++i) x[i] = fma(-sM[i * NV + k], x[k], x[i]);
-        if (k % 3 == 2) asm volatile("" ::: "memory");
-      }
-#pragma unroll
-      for (int k = 0; k < NV; ++k) x[k] *= sDm[k];
-#pragma unroll
-      for (int k = NV - 1; k >= 0; --k) {
-#pragma unroll
-        for (int i = 0; i < k; ++i) x[i] = fma(-sM[k * NV + i], x[k], x[i]);
-        if (k % 3 == 0) asm volatile("" ::: "memory");
-      }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) sX[i * NY1P + c] = x[i];
-#pragma unroll
-      for (int a = 0; a < NU; ++a) sU[a * NY1P + c] = (a == c) ? 1.0 : 0.0;
-    } else if (c < NY1P) {   // padding column: read by the 2x2 tiles, must be 0
-#pragma unroll
-      for (int i = 0; i < NV; ++i) sX[i * NY1P + c] = 0.0;
-#pragma unroll
-      for (int a = 0; a < NU; ++a) sU[a * NY1P + c] = 0.0;
-    }
-    wave_sync();
-  } else {
   // One lane per column c of [y; 1]; when two copies of the 32-lane column set fit the wave,
   // both halves solve for X (redundantly) and split the NU rows of U between them.
   constexpr bool kSplitU = 2 * NY1P <= kWave;
@@ -649,7 +576,74 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
       if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = 0.0;
   }
   wave_sync();
-  }   // TY
+  if constexpr (D::TY) {
+    // y = (u, z): X = M^-1 [B | Jc | -C] over all NV rows by block elimination on the base block.
+    // The code above left X_b = M_bb^-1 [-M_ba | Jc_b | -C_b] in rows 0..NB-1 and
+    // U = M_ab X_b + [M_aa | -Jc_a | C_a] in rows NB.. of sX; U's first NU columns are the Schur
+    // complement S = M_aa - M_ab M_bb^-1 M_ba.  Per column c:
+    //   S x_a = r_a' with r_a' = e_c (u columns) or -U[:, c] (contact / affine columns)
+    //   x_b = X_b[:, :NU] x_a (+ X_b[:, c] for c >= NU)
+    // Every lane factors S itself (registers, no synchronisation between pivot steps).
+    const int c = lane;
+    double xa[NU], xb[NB];
+    if (c < NY1) {
+      double Ls[NU][NU];
+#pragma unroll
+      for (int i = 0; i < NU; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Ls[i][j] = sU[i * NY1P + j];
+      double ds[NU];
+#pragma unroll
+      for (int k = 0; k < NU; ++k) {
+        ds[k] = recip1(Ls[k][k]);
+#pragma unroll
+        for (int i = k + 1; i < NU; ++i) {
+          const double lik = Ls[i][k] * ds[k];
+#pragma unroll
+          for (int j = k + 1; j <= i; ++j) Ls[i][j] = fma(-lik, Ls[j][k], Ls[i][j]);
+        }
+#pragma unroll
+        for (int i = k + 1; i < NU; ++i) Ls[i][k] *= ds[k];
+      }
+      const bool cu = c < NU;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const double u = sU[i * NY1P + c];
+        xa[i] = cu ? ((i == c) ? 1.0 : 0.0) : -u;
+      }
+#pragma unroll
+      for (int k = 0; k < NU; ++k)
+#pragma unroll
+        for (int i = k + 1; i < NU; ++i) xa[i] = fma(-Ls[i][k], xa[k], xa[i]);
+#pragma unroll
+      for (int k = 0; k < NU; ++k) xa[k] *= ds[k];
+#pragma unroll
+      for (int k = NU - 1; k >= 0; --k)
+#pragma unroll
+        for (int i = 0; i < k; ++i) xa[i] = fma(-Ls[k][i], xa[k], xa[i]);
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const double x0 = sX[r * NY1P + c];
+        double acc = cu ? 0.0 : x0;
+#pragma unroll
+        for (int q = 0; q < NU; ++q) acc = fma(sX[r * NY1P + q], xa[q], acc);
+        xb[r] = acc;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NU; ++i) xa[i] = 0.0;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) xb[r] = 0.0;
+    }
+    wave_sync();   // every lane has read X_b and U before any column is overwritten
+    if (c < NY1P) {
+#pragma unroll
+      for (int r = 0; r < NB; ++r) sX[r * NY1P + c] = xb[r];
+#pragma unroll
+      for (int i = 0; i < NU; ++i) sX[(NB + i) * NY1P + c] = xa[i];
+    }
+    wave_sync();
+  }
   // J, M, C dead from here on (R1, R2 get reused)
 
   STAMP_END(2);
@@ -755,7 +749,7 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
   double* w = ws + static_cast<size_t>(env) * D::WS;
   for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
   for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
-  for (int i = lane; i < NU * NY1P; i += kWave) w[D::W_U + i] = sU[i];
+  for (int i = lane; i < D::NUW * NY1P; i += kWave) w[D::W_U + i] = sU[i];
   for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
   STAMP_END(5);
   STAMP_STORE_SETUP();
@@ -938,7 +932,12 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
                 MI = D::MI, NRL = D::NRL;
   constexpr bool HRL = SMALL && hr_fits_lds<D>();
   using LY = IpmLayout<D, HRL>;
-  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * LY::IL];
+  // The one-wave variant must run ONE wavefront per SIMD: when its registers would allow two,
+  // the LDS request (> 160 KB / 5 per workgroup) is what keeps the dispatcher from stacking a
+  // fifth and sixth workgroup on some CUs while others idle (Go2 in torque coordinates: 26 KB
+  // of LDS, 255 VGPRs -> IPM 144 -> 158 us at 4,096 envs until padded).
+  constexpr int kLds = SMALL ? cmax(kEnvPerWave * LY::IL, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * LY::IL;
+  __shared__ __attribute__((aligned(16))) double sm[kLds];
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
   const int env_raw = blockIdx.x * kEnvPerWave + grp;

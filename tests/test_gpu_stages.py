@@ -4,7 +4,7 @@ reduction is computed:
   * x(y) satisfies the dynamics equality M dv + C - B u - Jc z = 0 for ANY y (autogen.py:87;
     checks X and U), in either reduced coordinate system the kernel uses:
       y = (dv_a, z): dv_b = X[y;1] (nb rows of X), dv_a = y_u, u = U[y;1]      (walter_sr)
-      y = (u, z):    dv = X[y;1] (nv rows of X), u = U[y;1] = y_u, U = [I | 0]  (unitree_go2)
+      y = (u, z):    dv = X[y;1] (nv rows of X), u = y_u, no U stored           (unitree_go2)
   * 1/2 y'Hr y + g'y differs from the full objective 1/2 x'Hx + f'x by a constant
     (checks Hr and g against H, f of autogen.py:304-319)
 """
@@ -41,11 +41,14 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     sz = nbytes.value // 8 // nenv
     ev = lambda a: (a + 1) // 2 * 2
     ny1p = ev(ny + 1)
+    # layout documented in include/osc_batch.h: [g | U | Hr | X], or [g | Hr | X] with nv rows
+    # of X in torque coordinates
     o_g, o_u = 0, ev(ny)
-    o_hr = o_u + nu * ny1p
+    ty = robot == "unitree_go2"                 # Dims<..., TY = true> in csrc/osc_batch.hip
+    nxr = nv if ty else nb
+    o_hr = o_u + (0 if ty else nu * ny1p)
     o_x = o_hr + ev(ny * ny)
-    nxr = (sz - o_x) // ny1p                     # layout documented in include/osc_batch.h
-    assert nxr in (nb, nv) and sz == o_x + nxr * ny1p
+    assert sz == o_x + nxr * ny1p
     dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     rc = L.osc_batch_assemble(s._h, nenv, *[p(a) for a in args], p(dbg), nbytes,
@@ -58,10 +61,8 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     for e in range(nenv):
         Hr = D[e, o_hr:o_hr + ny * ny].reshape(ny, ny)
         g = D[e, o_g:o_g + ny]
-        U = D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
+        U = np.eye(nu, ny + 1) if ty else D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
         X = D[e, o_x:].reshape(nxr, ny1p)[:, :ny + 1]
-        if nxr == nv:                           # torque coordinates: U = [I_nu | 0]
-            np.testing.assert_array_equal(U, np.eye(nu, ny + 1))
         np.testing.assert_array_equal(Hr, Hr.T)
         a = [inp[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a)

@@ -20,7 +20,10 @@ def run(path):
     L = ctypes.CDLL(path)
     vp = ctypes.c_void_p
     L.osc_batch_solve.argtypes = [vp, ctypes.c_int32] + [vp] * 10 + [vp, ctypes.c_size_t, vp]
+    only = os.environ.get("AB_ONLY")   # e.g. "unitree_go2:4096" (one configuration, for rocprof)
     for robot, nenv in (("unitree_go2", 4096), ("unitree_go2", 65536), ("walter_sr", 4096)):
+        if only and only != f"{robot}:{nenv}":
+            continue
         d = OscModelDesc()
         assert L.osc_desc_from_yaml(robot.encode(), config_path(robot).encode(), ctypes.byref(d)) == 0
         h = vp()
