@@ -400,6 +400,40 @@ __device__ __forceinline__ void upper_pair(int p, int& i, int& j) {
   j = p - start(r) + r;
 }
 
+// c += bcast_K(src) * m  in ONE instruction: v_fmac_f64_dpp with row_newbcast:K (the DPP
+// operand is read from lane K of each 16-lane row).  hipcc never forms this (64-bit DPP is
+// only legal with row_newbcast), hence inline asm.  The compiler's hazard recognizer cannot see
+// through inline asm, so every DPP read here carries its own guard: NOP = true prefixes
+// s_nop 1 (gfx9: a VALU write of the DPP source needs 2 wait states before the DPP read) for a
+// source just computed by the caller; NOP = false only where the source was written by one of
+// these asm statements several dependent instructions earlier.
+template <int K, bool NOP = false>
+__device__ __forceinline__ void fmac_bcast(double& c, double src, double m) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
+}
+template <int K, bool NOP = false>
+__device__ __forceinline__ void fmac_bcast_self(double& c, double m) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(m), "n"(K));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                 : "+v"(c) : "v"(m), "n"(K));
+}
+// Broadcast of lane K's v within each 16-lane row, guarded (v may have been written by asm).
+template <int K>
+__device__ __forceinline__ double bcast_guarded(double v) {
+  double r;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "=v"(r) : "v"(v), "n"(K));
+  return r;
+}
+
 // ============================ kernel 1: reduced QP per env ==================================
 template <class D>
 __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
@@ -583,66 +617,93 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     // complement S = M_aa - M_ab M_bb^-1 M_ba.  Per column c:
     //   S x_a = r_a' with r_a' = e_c (u columns) or -U[:, c] (contact / affine columns)
     //   x_b = X_b[:, :NU] x_a (+ X_b[:, c] for c >= NU)
-    // Every lane factors S itself (registers, no synchronisation between pivot steps).
+    // S = L D L' is factored once per 16-lane row (lane j holds column j; the four rows of the
+    // wave repeat it): pivot k's column is broadcast inside the row with v_fmac_f64_dpp
+    // row_newbcast, one instruction per trailing entry.  The solves then read L the same way --
+    // lane c of any row solves column c and takes L's entries from the row's lane k by DPP --
+    // so the factor never goes through LDS.  Every lane runs every step (a DPP read needs its
+    // source lane active); lanes past the last column compute garbage and write zeros.
+    static_assert(NU <= kRow, "TY: S fits one 16-lane row");
+    STAMP_END(2);
+    STAMP_BEGIN();
+    const int lj = lane & (kRow - 1);
+    double col[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) col[i] = sU[i * NY1P + (lj < NU ? lj : 0)];
+    double dj = 1.0;
+    static_for<0, NU>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      const double rk = recip1(bcast_guarded<k>(col[k]));       // 1 / S_k[k][k]
+      if (lj == k) dj = rk;
+      const double m = (lj > k) ? -col[k] * rk : 0.0;          // -S_k[k][j] / d_k, lanes j > k
+      static_for<k + 1, NU>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        fmac_bcast_self<k, true>(col[i], m);                    // S[i][j] -= S[i][k] S[k][j] / d_k
+      });
+    });
+    // lane j: col[i > j] = L[i][j] d_j (unscaled column), dj = 1 / d_j
+    double dinv[NU];
+    static_for<0, NU>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      dinv[k] = bcast_guarded<k>(dj);
+    });
+    STAMP_END(6);
+    STAMP_BEGIN();
     const int c = lane;
-    double xa[NU], xb[NB];
-    if (c < NY1) {
-      double Ls[NU][NU];
+    const bool cu = c < NU, live = c < NY1;
+    const int cc = (cu || !live) ? NU : c;   // a valid column to read for lanes that do not use it
+    double xa[NU], xb[NB], xbc[NB];
 #pragma unroll
-      for (int i = 0; i < NU; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j) Ls[i][j] = sU[i * NY1P + j];
-      double ds[NU];
-#pragma unroll
-      for (int k = 0; k < NU; ++k) {
-        ds[k] = recip1(Ls[k][k]);
-#pragma unroll
-        for (int i = k + 1; i < NU; ++i) {
-          const double lik = Ls[i][k] * ds[k];
-#pragma unroll
-          for (int j = k + 1; j <= i; ++j) Ls[i][j] = fma(-lik, Ls[j][k], Ls[i][j]);
-        }
-#pragma unroll
-        for (int i = k + 1; i < NU; ++i) Ls[i][k] *= ds[k];
-      }
-      const bool cu = c < NU;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        const double u = sU[i * NY1P + c];
-        xa[i] = cu ? ((i == c) ? 1.0 : 0.0) : -u;
-      }
-#pragma unroll
-      for (int k = 0; k < NU; ++k)
-#pragma unroll
-        for (int i = k + 1; i < NU; ++i) xa[i] = fma(-Ls[i][k], xa[k], xa[i]);
-#pragma unroll
-      for (int k = 0; k < NU; ++k) xa[k] *= ds[k];
-#pragma unroll
-      for (int k = NU - 1; k >= 0; --k)
-#pragma unroll
-        for (int i = 0; i < k; ++i) xa[i] = fma(-Ls[k][i], xa[k], xa[i]);
-#pragma unroll
-      for (int r = 0; r < NB; ++r) {
-        const double x0 = sX[r * NY1P + c];
-        double acc = cu ? 0.0 : x0;
-#pragma unroll
-        for (int q = 0; q < NU; ++q) acc = fma(sX[r * NY1P + q], xa[q], acc);
-        xb[r] = acc;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NU; ++i) xa[i] = 0.0;
-#pragma unroll
-      for (int r = 0; r < NB; ++r) xb[r] = 0.0;
+    for (int i = 0; i < NU; ++i) {
+      const double u = sU[i * NY1P + cc];
+      xa[i] = cu ? ((i == c) ? 1.0 : 0.0) : -u;
     }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      xb[r] = sX[r * NY1P + cc];                              // X_b[:, c] (contact / affine)
+      xbc[r] = sX[r * NY1P + (lj < NU ? lj : 0)];             // X_b[:, j]: the DPP source of lane j
+    }
+    // L z = r:  z[i] -= (L[i][k] d_k) (z[k] / d_k)
+    static_for<0, NU>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      const double t = -xa[k] * dinv[k];
+      static_for<k + 1, NU>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        fmac_bcast<k>(xa[i], col[i], t);
+      });
+    });
+#pragma unroll
+    for (int k = 0; k < NU; ++k) xa[k] *= dinv[k];
+    // L' x = y:  x[i] = y[i] - (1 / d_i) sum_{k > i} (L[k][i] d_i) x[k]
+    static_for<0, NU - 1>([&](auto J) {
+      constexpr int i = NU - 2 - decltype(J)::value;
+      double acc = 0.0;
+      static_for<i + 1, NU>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        fmac_bcast<i>(acc, col[k], xa[k]);
+      });
+      xa[i] = fma(-dinv[i], acc, xa[i]);
+    });
+    STAMP_END(7);
+    STAMP_BEGIN();
+    // x_b = X_b[:, :NU] x_a (+ X_b[:, c] for contact / affine columns)
+#pragma unroll
+    for (int r = 0; r < NB; ++r) xb[r] = cu ? 0.0 : xb[r];
+    static_for<0, NU>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) fmac_bcast<q>(xb[r], xbc[r], xa[q]);
+    });
     wave_sync();   // every lane has read X_b and U before any column is overwritten
     if (c < NY1P) {
 #pragma unroll
-      for (int r = 0; r < NB; ++r) sX[r * NY1P + c] = xb[r];
+      for (int r = 0; r < NB; ++r) sX[r * NY1P + c] = live ? xb[r] : 0.0;
 #pragma unroll
-      for (int i = 0; i < NU; ++i) sX[(NB + i) * NY1P + c] = xa[i];
+      for (int i = 0; i < NU; ++i) sX[(NB + i) * NY1P + c] = live ? xa[i] : 0.0;
     }
     wave_sync();
+    STAMP_END(8);
+    STAMP_BEGIN();
   }
   // J, M, C dead from here on (R1, R2 get reused)
 
@@ -756,36 +817,6 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
 }
 
 // ============================ kernel 2: interior point, 4 env / wave ========================
-
-// c += bcast_K(src) * m  in ONE instruction: v_fmac_f64_dpp with row_newbcast:K (the DPP
-// operand is read from lane K of each 16-lane row).  hipcc never forms this (64-bit DPP is
-// only legal with row_newbcast), hence inline asm.  The compiler's hazard recognizer cannot see
-// through inline asm, so every DPP read here carries its own guard: NOP = true prefixes
-// s_nop 1 (gfx9: a VALU write of the DPP source needs 2 wait states before the DPP read) for a
-// source just computed by the caller; NOP = false only where the source was written by one of
-// these asm statements several dependent instructions earlier.
-template <int K, bool NOP = false>
-__device__ __forceinline__ void fmac_bcast(double& c, double src, double m) {
-  if constexpr (NOP)
-    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
-  else
-    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(c) : "v"(src), "v"(m), "n"(K));
-}
-template <int K>
-__device__ __forceinline__ void fmac_bcast_self(double& c, double m) {
-  asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
-               : "+v"(c) : "v"(m), "n"(K));
-}
-// Broadcast of lane K's v within each 16-lane row, guarded (v may have been written by asm).
-template <int K>
-__device__ __forceinline__ double bcast_guarded(double v) {
-  double r;
-  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
-               : "=v"(r) : "v"(v), "n"(K));
-  return r;
-}
 
 // a += bcast_K(src) * ma;  b += bcast_K(src) * mb  (one broadcast source, two slots).
 // NOP = true guards a source that a VALU instruction may have written just before.

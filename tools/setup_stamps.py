@@ -17,7 +17,7 @@ from osc_amd.solver import OSCBatchSolver  # noqa: E402
 from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
 NAMES = ["A: stage inputs", "B: Ha = 2[J e]'W[J e]", "C: X, U (base block)", "D1: T1",
-         "D2: Hr | g", "write workspace"]
+         "D2: Hr | g", "write workspace", "C2 (TY): factor S", "C2: solve", "C2: x_b + write"]
 SLOTS = 12
 nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 for robot in ["unitree_go2", "walter_sr"]:
