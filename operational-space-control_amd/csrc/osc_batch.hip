@@ -1649,7 +1649,10 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 }
 
 using Go2 = Dims<18, 12, 4, 5, true>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites; y = (u, z)
-using Walter = Dims<14, 8, 8, 17>;    // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
+#ifndef OSC_WALTER_TY
+#define OSC_WALTER_TY 0
+#endif
+using Walter = Dims<14, 8, 8, 17, OSC_WALTER_TY>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
 
 enum KernelId { K_NONE = 0, K_GO2 = 1, K_WALTER = 2 };
 
