@@ -124,6 +124,7 @@ def ldl_solve(F, r):
     return sla.solve_triangular(L.T, z / d, lower=False, unit_diagonal=True)
 
 
+NU_STOP = 12   # torque entries of y in torque coordinates (Go2) for the "ustop" variant
 TRACE = None   # set to a list to record (it, mu, a_aff, a, alpha, sigma) per iteration
 
 
@@ -180,6 +181,7 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         lam = zr + (1.0 + ad if ad >= 0 else 0.0)
     eta = 0.99
     rp_c = None
+    last_du = None
     for it in range(max_iter + 1):
         for v in variant:
             if v.startswith("recenter") and it == int(v[8:]) and s @ lam / m > 1e-6:
@@ -197,6 +199,13 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         mu = s @ lam / m
         if mu <= eps_mu:
             return y, it, True
+        ustop = [v for v in variant if v.startswith("ustop")]
+        if ustop and last_du is not None:
+            # torque-coordinate stop: the last step moved the torques y[:NU] by less than
+            # tol * max(|u|, 1) while mu is already small ("ustop<tol>,<mu>")
+            tol, mth = (float(a) for a in ustop[0][5:].split(","))
+            if mu <= mth and last_du <= tol * max(np.abs(y[:NU_STOP]).max(), 1.0):
+                return y, it, True
         if it >= max_iter:
             return y, it, False
         pol = [float(v[6:]) for v in variant if v.startswith("polish")]
@@ -307,6 +316,7 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         if TRACE is not None:
             TRACE.append((it, mu, a_aff, a, alpha, sig, float(np.abs(rp).max()),
                           float(np.abs(rd).max())))
+        last_du = float(np.abs(alpha * dy[:NU_STOP]).max())
         y, s, lam = y + alpha * dy, s + alpha * ds, lam + alpha * dl
         if rp_c is not None:
             rp_c = (1.0 - alpha) * rp_c
