@@ -146,9 +146,12 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
 def run_mixed(args, world, rank, dev, barrier) -> None:
     """BASELINE configs[4]: mixed Go2 + WaLTER Sr.  Every rank solves its own shard of
     --nenv-per-gpu Go2 envs AND --nenv-per-gpu WaLTER envs (4,096 + 4,096 per GPU: 65,536 over 8
-    GPUs), the two models launched on two streams so their kernels overlap.  A
-    step = both shards solved; value = all envs of all ranks / max-over-ranks time."""
-    from osc_amd.solver import OSCBatchSolver
+    GPUs) in ONE osc_batch_solve_multi call: one assembly grid and one interior-point grid for
+    both models, WaLTER's wavefronts first so Go2's fill the SIMDs its early finishers free
+    (one kernel instantiation per model, no collective).  --mixed-mode streams /
+    serial run the two models as two osc_batch_solve calls on two streams / one stream instead.
+    A step = both shards solved; value = all envs of all ranks / max-over-ranks time."""
+    from osc_amd.solver import OSCBatchSolver, solve_multi_into
     nenv = args.nenv_per_gpu
     robots = ("unitree_go2", "walter_sr")
     main = torch.cuda.current_stream(dev)
@@ -158,13 +161,20 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
         solver = OSCBatchSolver(robot)
         d = generate(robot, nenv, shard_seed(rank) + 500 * i, args.scenario, args.mask)
         jobs.append((solver, solver.prepare(**d), solver.alloc_outputs(nenv)))
+    multi_jobs = [(s, o, inp) for s, inp, o in jobs]
 
     def step():
-        for st, (solver, inputs, out) in zip(streams, jobs):
-            st.wait_stream(main)
-            solver.solve_into(out, *inputs, stream=st)
-        for st in streams:
-            main.wait_stream(st)
+        if args.mixed_mode == "multi":
+            solve_multi_into(multi_jobs, stream=main)
+        elif args.mixed_mode == "serial":
+            for solver, inputs, out in jobs:
+                solver.solve_into(out, *inputs, stream=main)
+        else:
+            for st, (solver, inputs, out) in zip(streams, jobs):
+                st.wait_stream(main)
+                solver.solve_into(out, *inputs, stream=st)
+            for st in streams:
+                main.wait_stream(st)
 
     for _ in range(args.warmup):
         step()
@@ -197,10 +207,12 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
         "config": {"workload": f"mixed unitree_go2 + walter_sr {args.scenario} mask={args.mask}, "
                                f"{nenv} + {nenv} envs per GPU (BASELINE configs[4] at 8 GPUs)",
                    "robot": "mixed", "envs_per_gpu": 2 * nenv, "global_envs": stats.total_envs,
-                   "parallelism": f"env-shard x{world}, 2 streams per GPU"},
+                   "parallelism": f"env-shard x{world}, 2 models per GPU ({args.mixed_mode})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "osc_setup_kernel + osc_ipm_kernel x 2 models, 2 streams",
+                     "kernel": ("osc_setup_pair_kernel + osc_ipm_pair_kernel"
+                                if args.mixed_mode == "multi" else
+                                f"osc_setup_kernel + osc_ipm_kernel x 2 models ({args.mixed_mode})"),
                      "kernel_ms": stats.kernel_ms},
         "converged_frac": stats.converged}), flush=True)
 
@@ -291,6 +303,9 @@ def main() -> None:
     ap.add_argument("--mask-redraw", type=int, default=0,
                     help="cycle through this many Bernoulli masks, one per step (configs[3]: "
                          "contact-mode switching, walter_sr_true_tumbling_mjjoint.cc:554-614)")
+    ap.add_argument("--mixed-mode", default="multi", choices=["multi", "streams", "serial"],
+                    help="--robot mixed: one osc_batch_solve_multi call, or two solves on two "
+                         "streams / on one stream")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 

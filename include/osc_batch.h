@@ -173,6 +173,28 @@ int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
                                    double* warm_state, size_t warm_state_bytes,
                                    const void* workspace, size_t workspace_bytes, void* stream);
 
+/* One model's batch inside a multi-model call: the arguments of osc_batch_solve for that model
+ * (device pointers; `workspace` required, >= osc_workspace_bytes(model, nenv), 16-B aligned). */
+typedef struct {
+  const osc_model* model;
+  int32_t nenv;
+  const double *M, *C, *J, *b, *T, *contact_mask;
+  double* tau;
+  double* x;                      /* nullable */
+  int32_t* status;                /* nullable */
+  int32_t* iters;                 /* nullable */
+  void* workspace;
+  size_t workspace_bytes;
+} osc_batch_job;
+
+/* Several robots' batches on one GPU in one call (BASELINE configs[4]: Go2 + WaLTER Sr shards
+ * per GPU).  Results are bitwise those of one osc_batch_solve per job.  Two jobs of different
+ * kernels (unitree_go2 + walter_sr) whose batches each fit one wavefront per SIMD run as ONE
+ * assembly grid and ONE interior-point grid, the slower model's wavefronts first, so the other
+ * model's wavefronts fill the SIMDs freed by the first one's iteration-count tail; anything else
+ * runs the jobs one after another on `stream`. */
+int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, void* stream);
+
 /* Human-readable name of an osc_status. */
 const char* osc_status_string(int status);
 

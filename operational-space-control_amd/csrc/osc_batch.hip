@@ -435,15 +435,17 @@ __device__ __forceinline__ double bcast_guarded(double v) {
 }
 
 // ============================ kernel 1: reduced QP per env ==================================
+// The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
+// of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
+// grid: BASELINE configs[4]).
 template <class D>
-__global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
-    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
+__device__ __forceinline__ void setup_env(
+    const DevParams* __restrict__ P, int env, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
-    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
+    double* __restrict__ sm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
                 NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NA = D::NA;
-  __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
-  const int env = blockIdx.x;
   const int lane = threadIdx.x;
   if (env >= nenv) return;
 
@@ -816,6 +818,38 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
   STAMP_STORE_SETUP();
 }
 
+template <class D>
+__global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
+    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
+  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm);
+}
+
+// One model's arguments to a two-model launch.
+struct PairArgs {
+  const DevParams* P;
+  int nenv;
+  const double *M, *C, *J, *b, *T, *mask;
+  double* ws;
+  double *tau, *x;
+  int32_t *status, *iters;
+};
+
+// Two models' setup in one grid (BASELINE configs[4]: Go2 + WaLTER on one GPU): blocks
+// [0, A.nenv) are model A's envs, the rest model B's.  One launch, so the second model's
+// wavefronts fill the SIMDs the first model's leave, instead of two grids contending.
+template <class DA, class DB>
+__global__ __launch_bounds__(kWave, 2) void osc_setup_pair_kernel(PairArgs A, PairArgs B) {
+  __shared__ __attribute__((aligned(16))) double sm[cmax(DA::SMEM, DB::SMEM)];
+  const int blk = static_cast<int>(blockIdx.x);
+  if (blk < A.nenv)
+    setup_env<DA>(A.P, blk, A.nenv, A.M, A.C, A.J, A.b, A.T, A.mask, A.ws, sm);
+  else
+    setup_env<DB>(B.P, blk - A.nenv, B.nenv, B.M, B.C, B.J, B.b, B.T, B.mask, B.ws, sm);
+}
+
 // ============================ kernel 2: interior point, 4 env / wave ========================
 
 // a += bcast_K(src) * ma;  b += bcast_K(src) * mb  (one broadcast source, two slots).
@@ -953,25 +987,33 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
 
 // WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
 // is unchanged by it: the two-wave Go2 variant would otherwise spill more).
+// LDS doubles of one IPM wavefront.  The one-wave variant must run ONE wavefront per SIMD: when
+// its registers would allow two, the LDS request (> 160 KB / 5 per workgroup) is what keeps the
+// dispatcher from stacking a fifth and sixth workgroup on some CUs while others idle (Go2 in
+// torque coordinates: 26 KB of LDS, 255 VGPRs -> IPM 144 -> 158 us at 4,096 envs until padded).
+template <class D, bool SMALL>
+constexpr int ipm_lds_doubles() {
+  constexpr int il = IpmLayout<D, SMALL && hr_fits_lds<D>()>::IL;
+  return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
+}
+
+// The body of one IPM wavefront (envs 4 blk .. 4 blk + 3); `sm` is its ipm_lds_doubles<D, SMALL>
+// doubles of LDS.  Wrapped by osc_ipm_kernel (one model) and osc_ipm_pair_kernel (two models).
+// WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
+// is unchanged by it: the two-wave Go2 variant would otherwise spill more).
 template <class D, bool SMALL, bool WARM>
-__global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
-    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
+__device__ __forceinline__ void ipm_block(
+    const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
-    int fixup) {
+    int fixup, double* __restrict__ sm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
   constexpr bool HRL = SMALL && hr_fits_lds<D>();
   using LY = IpmLayout<D, HRL>;
-  // The one-wave variant must run ONE wavefront per SIMD: when its registers would allow two,
-  // the LDS request (> 160 KB / 5 per workgroup) is what keeps the dispatcher from stacking a
-  // fifth and sixth workgroup on some CUs while others idle (Go2 in torque coordinates: 26 KB
-  // of LDS, 255 VGPRs -> IPM 144 -> 158 us at 4,096 envs until padded).
-  constexpr int kLds = SMALL ? cmax(kEnvPerWave * LY::IL, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * LY::IL;
-  __shared__ __attribute__((aligned(16))) double sm[kLds];
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
-  const int env_raw = blockIdx.x * kEnvPerWave + grp;
+  const int env_raw = blk * kEnvPerWave + grp;
   const bool valid = env_raw < nenv;
   const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
   // Fix-up pass after a warm-started solve: only wavefronts holding an env that did not converge
@@ -988,8 +1030,8 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
   const double* __restrict__ wsw =
-      ws + static_cast<size_t>(blockIdx.x) * kEnvPerWave * D::WS + D::W_HR;   // L2-resident
-  const unsigned lane_off = static_cast<unsigned>(env - static_cast<int>(blockIdx.x) * kEnvPerWave) *
+      ws + static_cast<size_t>(blk) * kEnvPerWave * D::WS + D::W_HR;   // L2-resident
+  const unsigned lane_off = static_cast<unsigned>(env - blk * kEnvPerWave) *
                             static_cast<unsigned>(D::WS);
   double* sG = B + LY::I_G;
   double* sU = B + LY::I_U;
@@ -1648,6 +1690,36 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   }
 }
 
+template <class D, bool SMALL, bool WARM>
+__global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
+    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
+    int fixup) {
+  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL>()];
+  ipm_block<D, SMALL, WARM>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx, gstatus,
+                            giters, gwarm, fixup, sm);
+}
+
+// Two models' interior point in one grid, one wavefront per SIMD (the one-wave variant of both):
+// blocks [0, nbA) are model A's wavefronts, the rest model B's.  The dispatcher hands out blocks
+// in order, so with the slower model first the faster model's wavefronts fill the SIMDs that
+// the first model's early finishers free (its iteration-count tail) -- two grids on two streams
+// instead split the SIMDs between the models and each pays its own tail.
+template <class DA, class DB>
+__global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, PairArgs B) {
+  __shared__ __attribute__((aligned(16)))
+      double sm[cmax(ipm_lds_doubles<DA, true>(), ipm_lds_doubles<DB, true>())];
+  const int nbA = (A.nenv + kEnvPerWave - 1) / kEnvPerWave;
+  const int blk = static_cast<int>(blockIdx.x);
+  if (blk < nbA)
+    ipm_block<DA, true, false>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status, A.iters,
+                               nullptr, 0, sm);
+  else
+    ipm_block<DB, true, false>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x, B.status,
+                               B.iters, nullptr, 0, sm);
+}
+
 using Go2 = Dims<18, 12, 4, 5, true>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites; y = (u, z)
 #ifndef OSC_WALTER_TY
 #define OSC_WALTER_TY 0
@@ -1902,6 +1974,62 @@ extern "C" int osc_batch_assemble(const osc_model* model, int32_t nenv, const do
                                   size_t workspace_bytes, void* stream) {
   return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
                 workspace, workspace_bytes, stream, kAssemble);
+}
+
+namespace {
+
+template <class DA, class DB>
+void launch_pair(const osc_batch_job& a, const osc_batch_job& b, hipStream_t s) {
+  auto args = [](const osc_batch_job& j) {
+    PairArgs p;
+    p.P = j.model->dparams;
+    p.nenv = j.nenv;
+    p.M = j.M; p.C = j.C; p.J = j.J; p.b = j.b; p.T = j.T; p.mask = j.contact_mask;
+    p.ws = static_cast<double*>(j.workspace);
+    p.tau = j.tau; p.x = j.x; p.status = j.status; p.iters = j.iters;
+    return p;
+  };
+  const PairArgs A = args(a), B = args(b);
+  hipLaunchKernelGGL((osc_setup_pair_kernel<DA, DB>), dim3(static_cast<unsigned>(a.nenv + b.nenv)),
+                     dim3(kWave), 0, s, A, B);
+  const unsigned nb = static_cast<unsigned>((a.nenv + kEnvPerWave - 1) / kEnvPerWave +
+                                            (b.nenv + kEnvPerWave - 1) / kEnvPerWave);
+  hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB>), dim3(nb), dim3(kWave), 0, s, A, B);
+}
+
+}  // namespace
+
+extern "C" int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs)) return OSC_ERR_INVALID_ARGUMENT;
+  for (int i = 0; i < njobs; ++i) {   // every job checked before anything is launched
+    const osc_batch_job& j = jobs[i];
+    if (!j.model || j.nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
+    if (j.nenv == 0) continue;
+    if (!j.workspace || !j.contact_mask || !j.tau) return OSC_ERR_INVALID_ARGUMENT;
+    size_t need = 0;
+    osc_workspace_bytes(j.model, j.nenv, &need);
+    if (j.workspace_bytes < need || misaligned16(j.workspace) || misaligned16(j.contact_mask) ||
+        !j.M || !j.C || !j.J || !j.b || !j.T || misaligned16(j.M) || misaligned16(j.C) ||
+        misaligned16(j.J) || misaligned16(j.b) || misaligned16(j.T))
+      return OSC_ERR_INVALID_ARGUMENT;
+    if (j.model->kid == K_NONE) return OSC_ERR_UNSUPPORTED_DIMS;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (njobs == 2 && jobs[0].nenv > 0 && jobs[1].nenv > 0 && jobs[0].model->kid != jobs[1].model->kid &&
+      jobs[0].nenv <= jobs[0].model->small_batch_max && jobs[1].nenv <= jobs[1].model->small_batch_max) {
+    const bool a_walter = jobs[0].model->kid == K_WALTER;
+    const osc_batch_job& w = a_walter ? jobs[0] : jobs[1];   // slower per wavefront: first
+    const osc_batch_job& g = a_walter ? jobs[1] : jobs[0];
+    launch_pair<Walter, Go2>(w, g, s);
+    return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+  }
+  for (int i = 0; i < njobs; ++i) {
+    const osc_batch_job& j = jobs[i];
+    const int rc = launch(j.model, j.nenv, j.M, j.C, j.J, j.b, j.T, j.contact_mask, j.tau, j.x,
+                          j.status, j.iters, j.workspace, j.workspace_bytes, stream, kBoth);
+    if (rc != OSC_OK) return rc;
+  }
+  return OSC_OK;
 }
 
 extern "C" int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes) {

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_kin_model_dims", "osc_batch_kinematics", "osc_state_to_qpos",
                     "osc_qpos_workspace_bytes", "osc_batch_solve_qpos",
                     "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm",
-                    "osc_batch_solve_qpos_warm")
+                    "osc_batch_solve_qpos_warm", "osc_batch_solve_multi")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -51,6 +51,14 @@ class OscModelDesc(ctypes.Structure):
         ("eps_mu", ctypes.c_double),
         ("max_iter", ctypes.c_int32),
     ]
+
+
+class OscBatchJob(ctypes.Structure):
+    """osc_batch_job (include/osc_batch.h): one model's batch inside osc_batch_solve_multi."""
+    _fields_ = [("model", ctypes.c_void_p), ("nenv", ctypes.c_int32)] + \
+        [(n, ctypes.c_void_p) for n in ("M", "C", "J", "b", "T", "contact_mask", "tau", "x",
+                                         "status", "iters", "workspace")] + \
+        [("workspace_bytes", ctypes.c_size_t)]
 
 
 _B, _S = OSC_KIN_MAX_BODIES, OSC_KIN_MAX_SITES
@@ -124,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 6 + [ctypes.c_size_t, vp,
                                                                          ctypes.c_size_t, vp]
     L.osc_batch_solve_assembled_warm.restype = ctypes.c_int
+    L.osc_batch_solve_multi.argtypes = [ctypes.POINTER(OscBatchJob), i32, vp]
+    L.osc_batch_solve_multi.restype = ctypes.c_int
     kp = ctypes.POINTER(OscKinDesc)
     L.osc_kin_desc_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, kp]
     L.osc_kin_desc_from_json.restype = ctypes.c_int

@@ -188,3 +188,25 @@ class OSCBatchSolver:
         out = self.alloc_outputs(int(args[0].shape[0]), want_x)
         with torch.cuda.device(self.device):
             return self.solve_into(out, *args)
+
+
+def solve_multi_into(jobs, stream=None) -> None:
+    """osc_batch_solve_multi: several models' batches in one call on one stream (BASELINE
+    configs[4]: Go2 + WaLTER Sr per GPU).  `jobs` = [(solver, SolveResult, (M, C, J, b, T,
+    mask)), ...] with device tensors from solver.prepare / solver.alloc_outputs."""
+    arr = (_lib.OscBatchJob * len(jobs))()
+    ptr = lambda t: t.data_ptr() if t is not None else None
+    dev = None
+    for j, (solver, out, inputs) in zip(arr, jobs):
+        M, C, J, b, T, mask = inputs
+        j.model = solver._h.value
+        j.nenv = out.tau.shape[0]
+        j.M, j.C, j.J, j.b, j.T, j.contact_mask = (ptr(t) for t in (M, C, J, b, T, mask))
+        j.tau, j.x, j.status, j.iters = ptr(out.tau), ptr(out.x), ptr(out.status), ptr(out.iters)
+        j.workspace = ptr(out.workspace)
+        j.workspace_bytes = out.workspace.numel() * 8
+        dev = solver.device
+    s = (torch.cuda.current_stream(dev) if stream is None else stream).cuda_stream
+    rc = _lib.lib().osc_batch_solve_multi(arr, len(jobs), ctypes.c_void_p(s))
+    if rc != 0:
+        raise _lib.OSCError("osc_batch_solve_multi", rc)
