@@ -60,8 +60,16 @@ typedef struct {
   double ipos[OSC_KIN_MAX_BODIES][3];              /* body_ipos (COM, body frame)              */
   double iquat[OSC_KIN_MAX_BODIES][4];             /* body_iquat (principal axes)              */
   double inertia[OSC_KIN_MAX_BODIES][3];           /* body_inertia (principal moments)         */
-  int32_t site_body[OSC_KIN_MAX_SITES];            /* site_bodyid - 1                          */
+  int32_t site_body[OSC_KIN_MAX_SITES];            /* site_bodyid - 1: body carrying the point */
   double site_pos[OSC_KIN_MAX_SITES][3];           /* site_pos (body frame)                    */
+  /* Jacobian body of each task site: mj_jac / mj_jacDot take (point = site_xpos, body =
+   * body_ids[i]) (operational_space_controller.h:409-412), and body_ids comes from the config's
+   * body_list, not from the site.  With has_jac_body = 0 (zero-initialised descriptors) the
+   * Jacobian body is site_body; otherwise site_jac_body[k] (the point stays site k's, moving
+   * with that body at the current instant -- exactly mj_jac's semantics).  This is how the Go2
+   * controller's model-order site rows (osc.h:373) are reproduced: see osc_kin_desc_from_mjcf. */
+  int32_t has_jac_body;
+  int32_t site_jac_body[OSC_KIN_MAX_SITES];
 } osc_kin_desc;
 
 typedef struct osc_kin_model osc_kin_model;        /* opaque: descriptor + device tables */
@@ -70,6 +78,36 @@ typedef struct osc_kin_model osc_kin_model;        /* opaque: descriptor + devic
  * <robot>_kinematics.json schema).  `json_path` NULL = <robot>_kinematics.json next to the
  * library's config directory.  OSC_ERR_IO on a missing/malformed file. */
 int osc_kin_desc_from_json(const char* robot, const char* json_path, osc_kin_desc* desc);
+
+/* Host-only: fill `desc` from a MuJoCo MJCF file -- the reference's xml_path, which its
+ * controller loads with mj_loadXML (operational_space_controller.h:114-152).  The subset of
+ * MJCF that update_osc_data's quantities depend on is read: <compiler angle eulerseq>,
+ * <option gravity>, nested <default> classes (joint / site attributes, childclass / class),
+ * <body pos + quat | euler | axisangle | xyaxes | zaxis>, <inertial pos, orientation, mass,
+ * diaginertia | fullinertia>, <joint type="hinge" | "free" axis pos armature>, <freejoint>,
+ * <site pos>.  Geoms, actuators, sensors, contacts, visual/asset sections are skipped (they do
+ * not enter M, C, J, b).  Bodies are numbered in MuJoCo's depth-first order; sites likewise.
+ * Errors (OSC_ERR_IO): unreadable or malformed XML, a body without <inertial> (MuJoCo would
+ * infer it from geoms), slide / ball joints, more than one joint on a body, <include>/<frame>,
+ * unknown names.
+ * Task sites: task site k = (point, Jacobian body) with Jacobian body = body_names[k] and
+ *   site_order OSC_MJCF_SITES_BY_NAME:     point = the site named site_names[k]
+ *                                          (walter_sr: site_xpos(site_ids), W/osc.h:417);
+ *   site_order OSC_MJCF_SITES_MODEL_ORDER: point = the k-th site of the model
+ *                                          (unitree_go2: Map<Matrix<ns,3>>(site_xpos), G/osc.h:373:
+ *                                          rows 0..ns-1 in model order, names not consulted).
+ * body_names and site_names are the config's body_list and noncontact_site_list +
+ * contact_site_list (G/autogen.py:32-35); each name must exist in the model. */
+#define OSC_MJCF_SITES_BY_NAME 0
+#define OSC_MJCF_SITES_MODEL_ORDER 1
+int osc_kin_desc_from_mjcf(const char* xml_path, const char* const* body_names,
+                           const char* const* site_names, int32_t nsite, int32_t site_order,
+                           osc_kin_desc* desc);
+/* Same with the lists taken from the robot's YAML config (osc_desc_from_yaml's file; NULL = the
+ * default one) and the robot's own convention: "unitree_go2" model order, "walter_sr" /
+ * "walter_sr_wheels" by name. */
+int osc_kin_desc_from_mjcf_robot(const char* robot, const char* yaml_path, const char* xml_path,
+                                 osc_kin_desc* desc);
 
 /* Validate (tree order, joint types, sizes, positive masses / inertias, unit-normalisable
  * quaternions and axes), derive the kernel tables and upload them to the current HIP device. */

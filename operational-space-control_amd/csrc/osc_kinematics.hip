@@ -74,10 +74,11 @@ struct alignas(16) KinDev {   // alignas: sizeof % 16 == 0 (16-byte LDS staging)
   int32_t next_sibling[OSC_KIN_MAX_BODIES];
   uint32_t anc[OSC_KIN_MAX_BODIES];          // ancestor-or-self body mask
   int32_t dof_body[OSC_KIN_MAX_DOFS];
-  int32_t site_body[OSC_KIN_MAX_SITES];
+  int32_t site_body[OSC_KIN_MAX_SITES];      // body carrying the site point
+  int32_t site_jac[OSC_KIN_MAX_SITES];       // Jacobian body (mj_jac's body argument)
   uint32_t dof_relmask[OSC_KIN_MAX_DOFS];    // dofs j with M_ij structurally non-zero
   double dof_arm[OSC_KIN_MAX_DOFS];          // dof_armature
-  uint32_t site_dofmask[OSC_KIN_MAX_SITES];  // ancestor dofs of the site's body
+  uint32_t site_dofmask[OSC_KIN_MAX_SITES];  // ancestor dofs of the site's Jacobian body
   double gravity[3];
   double rq[OSC_KIN_MAX_BODIES][9];          // body_quat as a rotation (row-major)
   double pos[OSC_KIN_MAX_BODIES][3];
@@ -396,13 +397,13 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
   KIN_STOP(3);
   // ---- stage 4: sites (lane = site): world position, J-dot qvel ---------------------------
   for (int k = l; k < ns; k += kRow) {
-    const int bb = K->site_body[k];
-    const double* B = E + lay.body + kBodyStride * bb;
+    const double* Bp = E + lay.body + kBodyStride * K->site_body[k];   // point's body
+    const double* B = E + lay.body + kBodyStride * K->site_jac[k];      // Jacobian body
     const double* sp = K->site_pos[k];
     double xk[3];
     for (int i = 0; i < 3; ++i)
-      xk[i] = B[B_X + i] + B[B_R + 3 * i] * sp[0] + B[B_R + 3 * i + 1] * sp[1] +
-              B[B_R + 3 * i + 2] * sp[2];
+      xk[i] = Bp[B_X + i] + Bp[B_R + 3 * i] * sp[0] + Bp[B_R + 3 * i + 1] * sp[1] +
+              Bp[B_R + 3 * i + 2] * sp[2];
     double* Xs = E + lay.site + 3 * k;
     for (int i = 0; i < 3; ++i) Xs[i] = xk[i];
     const double w[3] = {B[B_W], B[B_W + 1], B[B_W + 2]};
@@ -616,6 +617,8 @@ int build_tables(const osc_kin_desc& d, KinDev* k) {
   for (int s = 0; s < d.nsite; ++s) {
     if (d.site_body[s] < 0 || d.site_body[s] >= d.nbody) return OSC_ERR_INVALID_ARGUMENT;
     k->site_body[s] = d.site_body[s];
+    k->site_jac[s] = d.has_jac_body ? d.site_jac_body[s] : d.site_body[s];
+    if (k->site_jac[s] < 0 || k->site_jac[s] >= d.nbody) return OSC_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < 3; ++i) k->site_pos[s][i] = d.site_pos[s][i];
   }
   for (int i = 0; i < 3; ++i) k->gravity[i] = d.gravity[i];
@@ -628,7 +631,7 @@ int build_tables(const osc_kin_desc& d, KinDev* k) {
   for (int i = 0; i < nv; ++i) k->dof_arm[i] = k->arm[k->dof_body[i]];
   for (int s = 0; s < d.nsite; ++s)
     for (int j = 0; j < nv; ++j)
-      if ((k->anc[k->site_body[s]] >> k->dof_body[j]) & 1u) k->site_dofmask[s] |= 1u << j;
+      if ((k->anc[k->site_jac[s]] >> k->dof_body[j]) & 1u) k->site_dofmask[s] |= 1u << j;
   k->nbody = d.nbody;
   k->nq = nq;
   k->nv = nv;
@@ -814,6 +817,13 @@ extern "C" int osc_kin_desc_from_json(const char* robot, const char* json_path,
     if (!jnum(S.get("body"), &body) || !jnums(S.get("pos"), desc->site_pos[s], 3))
       return OSC_ERR_IO;
     desc->site_body[s] = static_cast<int32_t>(body);
+    desc->site_jac_body[s] = desc->site_body[s];
+    if (const JVal* jb = S.get("jac_body")) {   // optional: Jacobian body != the site's body
+      double v = 0.0;
+      if (!jnum(jb, &v)) return OSC_ERR_IO;
+      desc->site_jac_body[s] = static_cast<int32_t>(v);
+      desc->has_jac_body = 1;
+    }
   }
   return OSC_OK;
 }

@@ -219,6 +219,28 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   return OSC_OK;
 }
 
+// The config's body_list and noncontact_site_list + contact_site_list (autogen.py:32-35), for the
+// MJCF reader (osc_mjcf.cpp: osc_kin_desc_from_mjcf_robot).  Same file and checks as above.
+int osc_config_lists(const char* robot, const char* yaml_path, std::vector<std::string>* bodies,
+                     std::vector<std::string>* sites) {
+  osc_model_desc d;
+  int rc = osc_desc_from_yaml(robot, yaml_path, &d);   // validates the lists against the robot
+  if (rc != OSC_OK) return rc;
+  const RobotInfo* info = nullptr;
+  for (const auto& r : registry())
+    if (std::strcmp(r.name, robot) == 0) info = &r;
+  std::string path = yaml_path ? std::string(yaml_path)
+                               : library_dir() + "/../config/" + info->default_config;
+  std::ifstream in(path);
+  MiniYaml y;
+  std::string err;
+  if (!in || !y.parse(in, &err)) return OSC_ERR_IO;
+  *bodies = y.lists["body_list"];
+  *sites = y.lists["noncontact_site_list"];
+  for (const auto& c : y.lists["contact_site_list"]) sites->push_back(c);
+  return OSC_OK;
+}
+
 extern "C" const char* osc_status_string(int status) {
   switch (status) {
     case OSC_OK: return "OSC_OK";

@@ -29,7 +29,8 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_kin_model_dims", "osc_batch_kinematics", "osc_state_to_qpos",
                     "osc_qpos_workspace_bytes", "osc_batch_solve_qpos",
                     "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm",
-                    "osc_batch_solve_qpos_warm", "osc_batch_solve_multi")
+                    "osc_batch_solve_qpos_warm", "osc_batch_solve_multi",
+                    "osc_kin_desc_from_mjcf", "osc_kin_desc_from_mjcf_robot")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -76,6 +77,7 @@ class OscKinDesc(ctypes.Structure):
         ("ipos", (ctypes.c_double * 3) * _B), ("iquat", (ctypes.c_double * 4) * _B),
         ("inertia", (ctypes.c_double * 3) * _B),
         ("site_body", ctypes.c_int32 * _S), ("site_pos", (ctypes.c_double * 3) * _S),
+        ("has_jac_body", ctypes.c_int32), ("site_jac_body", ctypes.c_int32 * _S),
     ]
 
 
@@ -137,6 +139,12 @@ def lib() -> ctypes.CDLL:
     kp = ctypes.POINTER(OscKinDesc)
     L.osc_kin_desc_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, kp]
     L.osc_kin_desc_from_json.restype = ctypes.c_int
+    L.osc_kin_desc_from_mjcf.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                         ctypes.POINTER(ctypes.c_char_p), i32, i32, kp]
+    L.osc_kin_desc_from_mjcf.restype = ctypes.c_int
+    L.osc_kin_desc_from_mjcf_robot.argtypes = [ctypes.c_char_p, ctypes.c_char_p,
+                                               ctypes.c_char_p, kp]
+    L.osc_kin_desc_from_mjcf_robot.restype = ctypes.c_int
     L.osc_kin_model_create.argtypes = [kp, ctypes.POINTER(vp)]
     L.osc_kin_model_create.restype = ctypes.c_int
     L.osc_kin_model_create_from_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p,
@@ -202,4 +210,49 @@ def kin_desc_from_dict(tree: dict) -> OscKinDesc:
     for k, s in enumerate(sites):
         d.site_body[k] = s["body"]
         d.site_pos[k][:] = s["pos"]
+        d.site_jac_body[k] = s.get("jac_body", s["body"])
+        if "jac_body" in s:
+            d.has_jac_body = 1
+    return d
+
+
+def kin_desc_to_dict(d: OscKinDesc, name: str = "") -> dict:
+    """The <robot>_kinematics.json schema of a descriptor (inverse of kin_desc_from_dict)."""
+    jt = {JOINT_FREE: "free", JOINT_HINGE: "hinge", JOINT_NONE: "none"}
+    bodies = []
+    for i in range(d.nbody):
+        bodies.append({"parent": d.parent[i], "joint": jt[d.jnt_type[i]], "pos": list(d.pos[i]),
+                       "quat": list(d.quat[i]), "axis": list(d.axis[i]),
+                       "jnt_pos": list(d.jnt_pos[i]), "armature": d.armature[i],
+                       "mass": d.mass[i], "ipos": list(d.ipos[i]), "iquat": list(d.iquat[i]),
+                       "diaginertia": list(d.inertia[i])})
+    sites = []
+    for k in range(d.nsite):
+        s = {"body": d.site_body[k], "pos": list(d.site_pos[k])}
+        if d.has_jac_body:
+            s["jac_body"] = d.site_jac_body[k]
+        sites.append(s)
+    return {"name": name, "gravity": list(d.gravity), "bodies": bodies, "sites": sites}
+
+
+def kin_desc_from_mjcf(xml_path: str, body_names, site_names, model_order: bool) -> OscKinDesc:
+    """osc_kin_desc_from_mjcf (host-only MJCF reader; include/osc_kinematics.h)."""
+    d = OscKinDesc()
+    n = len(site_names)
+    bn = (ctypes.c_char_p * n)(*[x.encode() for x in body_names])
+    sn = (ctypes.c_char_p * n)(*[x.encode() for x in site_names])
+    rc = lib().osc_kin_desc_from_mjcf(xml_path.encode(), bn, sn, n, 1 if model_order else 0,
+                                      ctypes.byref(d))
+    if rc != 0:
+        raise OSCError("osc_kin_desc_from_mjcf", rc)
+    return d
+
+
+def kin_desc_from_mjcf_robot(robot: str, xml_path: str, yaml_path: str | None = None) -> OscKinDesc:
+    d = OscKinDesc()
+    rc = lib().osc_kin_desc_from_mjcf_robot(robot.encode(),
+                                            yaml_path.encode() if yaml_path else None,
+                                            xml_path.encode(), ctypes.byref(d))
+    if rc != 0:
+        raise OSCError("osc_kin_desc_from_mjcf_robot", rc)
     return d

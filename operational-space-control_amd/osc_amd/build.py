@@ -3,7 +3,7 @@ loader) and libosc_controller.so (the OperationalSpaceController shim over the C
 
     python -m osc_amd.build          (from operational-space-control_amd/)
 
-Plain hipcc, no cmake: four translation units.  The .so files land in
+Plain hipcc, no cmake: five translation units.  The .so files land in
 operational-space-control_amd/lib/ so that it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
@@ -20,7 +20,8 @@ OUT_CTRL = os.path.join(PKG_DIR, "lib", "libosc_controller.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_producers.hip", "osc_kinematics.hip"]
+SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_mjcf.cpp", "osc_producers.hip",
+           "osc_kinematics.hip"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:

@@ -206,12 +206,15 @@ def kinematics(m: KinModel, qpos, qvel):
     for k, s in enumerate(m.sites):
         bi = s["body"]
         x = xpos[bi] + xmat[bi] @ np.asarray(s["pos"])
-        Jp, Jr = point_jacobian(m, fk, bi, x)
+        # mj_jac(point, body_ids[k]): the point is the site's, the rigid motion is the Jacobian
+        # body's (unitree_go2/operational_space_controller.h:409-412; "jac_body" absent = same)
+        jb = s.get("jac_body", bi)
+        Jp, Jr = point_jacobian(m, fk, jb, x)
         J[3 * k:3 * k + 3] = Jp
         J[3 * ns + 3 * k:3 * ns + 3 * k + 3] = Jr
-        _, a = accel(bi, x)
+        _, a = accel(jb, x)
         bb[3 * k:3 * k + 3] = a
-        bb[3 * ns + 3 * k:3 * ns + 3 * k + 3] = al[bi]
+        bb[3 * ns + 3 * k:3 * ns + 3 * k + 3] = al[jb]
     return M, C, J, bb
 
 

@@ -19,10 +19,21 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-12
 
 
+def _mjcf_tree(robot):
+    """config/<robot>.xml through the MJCF reader with the robot's site convention: Go2 in
+    model order (its task sites' points and Jacobian bodies differ, G/osc.h:373), WaLTER by
+    name (W/osc.h:417)."""
+    import os
+    from osc_amd.mjcf import load_mjcf_robot
+    from osc_amd.kinematics import kin_json_path
+    return load_mjcf_robot(robot, os.path.join(os.path.dirname(kin_json_path(robot)), f"{robot}.xml"))
+
+
 def _trees():
     return {"unitree_go2": load_tree("unitree_go2"), "walter_sr": load_tree("walter_sr"),
             "random_free": random_tree(5), "random_fixed": random_tree(6, free_root=False),
-            "chain16": chain_tree(7)}
+            "chain16": chain_tree(7), "unitree_go2_mjcf": _mjcf_tree("unitree_go2"),
+            "walter_sr_mjcf": _mjcf_tree("walter_sr")}
 
 
 TREES = _trees()
