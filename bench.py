@@ -283,7 +283,33 @@ def baseline_config_tag(args, nenv):
     return f" (BASELINE configs[{c}])" if c is not None else ""
 
 
-def main() -> None:
+class DeviceClock:
+    """HIP events on the launch stream on a GPU; host timestamps on the CPU (the gloo test of the
+    multi-rank path, tests/test_dist.py, runs the same per-rank code without a device)."""
+
+    class _HostEvent:
+        def record(self, stream=None):
+            self.t = time.perf_counter()
+
+        def elapsed_time(self, other):
+            return (other.t - self.t) * 1e3
+
+    def __init__(self, dev: torch.device):
+        self.cuda = dev.type == "cuda"
+        self.dev = dev
+
+    def event(self):
+        return torch.cuda.Event(enable_timing=True) if self.cuda else self._HostEvent()
+
+    def sync(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+
+    def stream(self):
+        return torch.cuda.current_stream(self.dev) if self.cuda else None
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -300,6 +326,9 @@ def main() -> None:
                     help="skip the warm-start (random-walk) timing reported beside the headline")
     ap.add_argument("--no-front-end", action="store_true",
                     help="skip the kinematics front-end timing (reported beside the headline)")
+    ap.add_argument("--no-single-env", action="store_true",
+                    help="skip the configs[0] single-env tick latency reported beside the headline")
+    ap.add_argument("--single-env-ticks", type=int, default=2000)
     ap.add_argument("--mask-redraw", type=int, default=0,
                     help="cycle through this many Bernoulli masks, one per step (configs[3]: "
                          "contact-mode switching, walter_sr_true_tumbling_mjjoint.cc:554-614)")
@@ -307,7 +336,165 @@ def main() -> None:
                     help="--robot mixed: one osc_batch_solve_multi call, or two solves on two "
                          "streams / on one stream")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_ranks(args, argv) -> int | None:
+    """One process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process IS a rank
+    and WORLD_SIZE must equal --gpus.  Otherwise --gpus N > 1 starts the N ranks itself: a
+    torch.distributed.run child on 127.0.0.1 running this script with the same arguments, started
+    before this process has touched the GPU; its exit code is returned."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver_cls,
+                 clock: DeviceClock):
+    """The timed region of one rank (BASELINE metric): warmup, barrier, K steps of assemble +
+    interior point over this rank's shard, barrier, then the max-over-ranks reduction.  Returns
+    (line, solver, inputs) on rank 0 and (None, solver, inputs) elsewhere."""
+    nenv = args.nenv_per_gpu
+    solver = solver_cls(args.robot)
+    d = generate(args.robot, nenv, shard_seed(rank), args.scenario, args.mask)
+    inputs = solver.prepare(**d)
+    out = solver.alloc_outputs(nenv)
+    stream = clock.stream()
+    # per-step contact masks (mask switching): step k assembles and solves with masks[k % K]
+    masks = [inputs[5]]
+    if args.mask_redraw > 0:
+        rng = np.random.default_rng(shard_seed(rank) + 1)
+        nc = inputs[5].shape[1]
+        masks = [torch.from_numpy((rng.uniform(size=(nenv, nc)) < 0.75).astype(np.float64))
+                 .to(dev) for _ in range(args.mask_redraw)]
+
+    for _ in range(args.warmup):
+        solver.solve_into(out, *inputs)
+    clock.sync()
+
+    # Each step = osc_batch_assemble (setup kernel) + osc_batch_solve_assembled (interior-point
+    # kernel), the two halves of osc_batch_solve, with HIP events on the launch stream around
+    # each kernel.
+    ev = [[clock.event() for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    clock.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        mask = masks[k % len(masks)]
+        ev[k][0].record(stream)
+        solver.assemble_into(out, *inputs[:5], mask)
+        ev[k][1].record(stream)
+        solver.solve_assembled_into(out, mask)
+        ev[k][2].record(stream)
+    clock.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+
+    st = out.status.cpu().numpy()
+    mean_iters = float(out.iters.double().mean().item())
+    stats = reduce_stats(world, dev, nenv, elapsed, setup_ms, ipm_ms, int((st == 0).sum()))
+    elapsed, kernel_ms, setup_ms, ipm_ms = stats.elapsed_s, stats.kernel_ms, stats.setup_ms, stats.ipm_ms
+    if rank != 0:
+        return None, solver, inputs
+    total = stats.total_envs
+    value = job_value(stats, args.steps)
+    bps = bytes_per_solve(args.robot)
+    # dominant kernel = osc_ipm_kernel (~80 % of the solve): path bytes per launch over its
+    # own event-timed duration; the setup + IPM pair is reported beside it
+    achieved = bps * nenv / (ipm_ms * 1e-3) / 1e9
+    achieved_pair = bps * nenv / (kernel_ms * 1e-3) / 1e9
+    traffic = traffic_pair = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as fh:
+            tj = json.load(fh)
+        if tj.get("robot") == args.robot and tj.get("nenv") == nenv:
+            traffic_pair = tj.get("bytes_per_launch")
+            traffic = tj.get("per_kernel", {}).get("osc_ipm_kernel")
+    flops = algorithmic_flops(args.robot, mean_iters)
+    tflops = flops * nenv / (kernel_ms * 1e-3) / 1e12
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded post-kinematics M, C, J, b, T, mask; osc_amd.synth)",
+        "config": {"workload": f"{args.robot} {args.scenario} mask={args.mask}"
+                               f"{f' redrawn per step ({args.mask_redraw} masks)' if args.mask_redraw else ''}, "
+                               f"{nenv} envs per GPU{baseline_config_tag(args, nenv)}",
+                   "robot": args.robot, "envs_per_gpu": nenv, "global_envs": total,
+                   "parallelism": f"env-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
+                     "bytes_per_solve": bps,
+                     "inputs": "cache-warm: the same batch every step (its 31 MB stays in the "
+                               "256 MB Infinity Cache); the kernel is latency-bound",
+                     "solve_pair": {"kernel": "osc_setup_kernel + osc_ipm_kernel",
+                                    "kernel_ms": kernel_ms, "achieved": achieved_pair,
+                                    "frac": achieved_pair / HBM_PEAK_GBS,
+                                    "traffic": traffic_pair,
+                                    "kernel_ms_split": {"osc_setup_kernel": setup_ms,
+                                                        "osc_ipm_kernel": ipm_ms}}},
+        "roofline_fp64": {"kernel": "osc_setup_kernel + osc_ipm_kernel", "achieved": tflops,
+                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": tflops / FP64_PEAK_TFLOPS,
+                          "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
+        "converged_frac": stats.converged,
+    }
+    return line, solver, inputs
+
+
+def single_env(robot: str, ticks: int) -> dict:
+    """BASELINE configs[0]: one environment, one tick at a time through the controller
+    (osc_amd/bin/osc_tick_latency: OperationalSpaceController::step() = State packing, H2D, GPU
+    kinematics + QP, D2H), against the reference's 2,000 us control period (osc.h:108).
+    Reported beside the CPU port's single-core rate; never part of `value`."""
+    import subprocess
+    exe = os.path.join(REPO, "operational-space-control_amd", "bin", "osc_tick_latency")
+    xml = os.path.join(REPO, "operational-space-control_amd", "config",
+                       f"{'unitree_go2' if robot == 'unitree_go2' else 'walter_sr'}.xml")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} not built (__graft_entry__.build())"}
+    r = subprocess.run([exe, robot, xml, str(ticks)], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": f"osc_tick_latency exit {r.returncode}: {r.stderr.strip()[-300:]}"}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["path"] = ("OperationalSpaceController::step(): State -> qpos/qvel, H2D, GPU kinematics "
+                   "(MJCF tree) + reduced QP + interior point (warm), D2H; wall time per tick")
+    res["reference_period_us"] = 2000
+    return res
+
+
+def main(argv=None) -> None:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    rc = launch_ranks(args, argv)
+    if rc is not None:
+        sys.exit(rc)
 
     ri = rank_info()
     world, rank, local = ri.world, ri.rank, ri.local
@@ -327,108 +514,19 @@ def main() -> None:
         return
 
     from osc_amd.solver import OSCBatchSolver
-    nenv = args.nenv_per_gpu
-    solver = OSCBatchSolver(args.robot)
-    d = generate(args.robot, nenv, shard_seed(rank), args.scenario, args.mask)
-    inputs = solver.prepare(**d)
-    out = solver.alloc_outputs(nenv)
-    stream = torch.cuda.current_stream(dev)
-    # per-step contact masks (mask switching): step k assembles and solves with masks[k % K]
-    masks = [inputs[5]]
-    if args.mask_redraw > 0:
-        rng = np.random.default_rng(shard_seed(rank) + 1)
-        nc = inputs[5].shape[1]
-        masks = [torch.from_numpy((rng.uniform(size=(nenv, nc)) < 0.75).astype(np.float64))
-                 .to(dev) for _ in range(args.mask_redraw)]
-
-    for _ in range(args.warmup):
-        solver.solve_into(out, *inputs)
-    torch.cuda.synchronize()
-
-    # Each step = osc_batch_assemble (setup kernel) + osc_batch_solve_assembled (interior-point
-    # kernel), the two halves of osc_batch_solve, with HIP events on the launch stream around
-    # each kernel.
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        mask = masks[k % len(masks)]
-        ev[k][0].record(stream)
-        solver.assemble_into(out, *inputs[:5], mask)
-        ev[k][1].record(stream)
-        solver.solve_assembled_into(out, mask)
-        ev[k][2].record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
-    kernel_ms = setup_ms + ipm_ms
-
-    st = out.status.cpu().numpy()
-    mean_iters = float(out.iters.double().mean().item())
-    stats = reduce_stats(world, dev, nenv, elapsed, setup_ms, ipm_ms, int((st == 0).sum()))
-    elapsed, kernel_ms, setup_ms, ipm_ms = stats.elapsed_s, stats.kernel_ms, stats.setup_ms, stats.ipm_ms
-    converged = stats.converged
-
-    if rank == 0:
-        total = stats.total_envs
-        value = job_value(stats, args.steps)
-        bps = bytes_per_solve(args.robot)
-        # dominant kernel = osc_ipm_kernel (~88 % of the solve): path bytes per launch over its
-        # own event-timed duration; the setup + IPM pair is reported beside it
-        achieved = bps * nenv / (ipm_ms * 1e-3) / 1e9
-        achieved_pair = bps * nenv / (kernel_ms * 1e-3) / 1e9
-        traffic = traffic_pair = None
-        if os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as fh:
-                tj = json.load(fh)
-            if tj.get("robot") == args.robot and tj.get("nenv") == nenv:
-                traffic_pair = tj.get("bytes_per_launch")
-                traffic = tj.get("per_kernel", {}).get("osc_ipm_kernel")
-        flops = algorithmic_flops(args.robot, mean_iters)
-        tflops = flops * nenv / (kernel_ms * 1e-3) / 1e12
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "solves/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (seeded post-kinematics M, C, J, b, T, mask; osc_amd.synth)",
-            "config": {"workload": f"{args.robot} {args.scenario} mask={args.mask}"
-                                   f"{f' redrawn per step ({args.mask_redraw} masks)' if args.mask_redraw else ''}, "
-                                   f"{nenv} envs per GPU{baseline_config_tag(args, nenv)}",
-                       "robot": args.robot, "envs_per_gpu": nenv, "global_envs": total,
-                       "parallelism": f"env-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
-                         "bytes_per_solve": bps,
-                         "solve_pair": {"kernel": "osc_setup_kernel + osc_ipm_kernel",
-                                        "kernel_ms": kernel_ms, "achieved": achieved_pair,
-                                        "frac": achieved_pair / HBM_PEAK_GBS,
-                                        "traffic": traffic_pair,
-                                        "kernel_ms_split": {"osc_setup_kernel": setup_ms,
-                                                            "osc_ipm_kernel": ipm_ms}}},
-            "roofline_fp64": {"kernel": "osc_setup_kernel + osc_ipm_kernel", "achieved": tflops,
-                              "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": tflops / FP64_PEAK_TFLOPS,
-                              "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
-            "converged_frac": converged,
-        }
+    clock = DeviceClock(dev)
+    line, solver, inputs = run_headline(args, world, rank, dev, barrier, OSCBatchSolver, clock)
+    if line is not None:
+        nenv = args.nenv_per_gpu
+        stream = clock.stream()
         if world == 1 and not args.no_warm:
             line["warm"] = warm_ticks(solver, inputs, nenv, args.steps, args.warmup,
                                       shard_seed(rank) + 7, stream)
         if world == 1 and not args.no_front_end:   # rank-local extra; N=1 only, like cpu_baseline
             line["front_end"] = front_end(args.robot, solver, nenv, args.steps, args.warmup,
                                           shard_seed(rank), stream)
+        if world == 1 and not args.no_single_env:
+            line["single_env"] = single_env(args.robot, args.single_env_ticks)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.robot, args.cpu_seconds, args.cpu_cores)
         print(json.dumps(line), flush=True)

@@ -93,8 +93,11 @@ class OperationalSpaceController {
    * (empty = the robot's default config); control_rate_us as the reference (default 2000). */
   OperationalSpaceController(std::string robot, std::string yaml_path, KinematicsFn kinematics,
                              int control_rate_us = 2000);
-  /* GPU kinematics front end: kin_json_path = the kinematic tree (empty = the robot's default
-   * <robot>_kinematics.json next to the library's config directory). */
+  /* GPU kinematics front end: kin_json_path = the kinematic tree -- an MJCF file (*.xml, read by
+   * osc_kin_desc_from_mjcf_robot with the robot's config lists, as the reference loads its
+   * xml_path, operational_space_controller.h:114-152) or a tree JSON (empty = the robot's
+   * default <robot>_kinematics.json next to the library's config directory).  The file is read
+   * by initialize(); a load failure is InternalError("Failed to load Mujoco Model") (:117). */
   explicit OperationalSpaceController(std::string robot, std::string yaml_path = "",
                                       int control_rate_us = 2000, std::string kin_json_path = "");
   ~OperationalSpaceController();
@@ -135,6 +138,7 @@ class OperationalSpaceController {
   KinematicsFn kinematics_;
   bool gpu_kinematics_ = false;
   osc_kin_model* kin_ = nullptr;
+  osc_kin_desc kin_desc_{};          // read by initialize(), uploaded by initialize_optimization()
   int nq_ = 0;
   int control_rate_us_;
   osc_model_desc desc_{};

@@ -68,6 +68,19 @@ Status OperationalSpaceController::initialize(State initial_state) {
   if (initial_state.contact_mask.size() != static_cast<size_t>(nc_))
     return InvalidArgumentError("State.contact_mask must have one entry per contact site");
   if (!kinematics_ && !gpu_kinematics_) return InvalidArgumentError("no kinematics provider");
+  if (gpu_kinematics_) {
+    // the reference loads the robot's MJCF here and resolves its sites / bodies (:114-152)
+    const std::string& p = kin_json_path_;
+    const bool mjcf = p.size() >= 4 && p.compare(p.size() - 4, 4, ".xml") == 0;
+    // the wheel-weight config drives the same robot as walter_sr
+    const std::string tree = robot_ == "walter_sr_wheels" ? "walter_sr" : robot_;
+    const int krc = mjcf ? osc_kin_desc_from_mjcf_robot(robot_.c_str(),
+                                                        yaml_path_.empty() ? nullptr : yaml_path_.c_str(),
+                                                        p.c_str(), &kin_desc_)
+                         : osc_kin_desc_from_json(tree.c_str(), p.empty() ? nullptr : p.c_str(),
+                                                  &kin_desc_);
+    if (krc != OSC_OK) return InternalError("Failed to load Mujoco Model");
+  }
   if (gpu_kinematics_ &&
       (initial_state.motor_position.size() != static_cast<size_t>(nu_) ||
        initial_state.motor_velocity.size() != static_cast<size_t>(nu_) ||
@@ -92,11 +105,7 @@ Status OperationalSpaceController::initialize_optimization() {
   size_t in_doubles = even(nv_ * nv_) + even(nv_) + even(s * nv_) + even(s) +
                       even(ns_ * 6) + even(nc_);
   if (gpu_kinematics_) {
-    // the wheel-weight config drives the same robot as walter_sr
-    const std::string tree = robot_ == "walter_sr_wheels" ? "walter_sr" : robot_;
-    st = from_osc(osc_kin_model_create_from_json(
-                      tree.c_str(), kin_json_path_.empty() ? nullptr : kin_json_path_.c_str(), &kin_),
-                  "osc_kin_model_create_from_json");
+    st = from_osc(osc_kin_model_create(&kin_desc_, &kin_), "osc_kin_model_create");
     if (!st.ok()) {
       release_device();
       return st;

@@ -31,6 +31,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         t_out = os.path.getmtime(OUT)
         if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):
             build_controller()
+            build_tick_latency()
             return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [HIPCC, "-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared",
@@ -41,7 +42,26 @@ def build(verbose: bool = False, force: bool = False) -> str:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     build_controller(force=True)
+    build_tick_latency(force=True)
     return OUT
+
+
+OUT_TICK = os.path.join(PKG_DIR, "bin", "osc_tick_latency")
+
+
+def build_tick_latency(force: bool = False) -> str:
+    """Host program timing single-env ticks through the controller (BASELINE configs[0])."""
+    src = os.path.join(CSRC, "osc_tick_latency.cpp")
+    deps = [src, OUT_CTRL, os.path.join(REPO, "include", "osc_controller.h")]
+    if not force and os.path.exists(OUT_TICK) and \
+            all(os.path.getmtime(p) <= os.path.getmtime(OUT_TICK) for p in deps):
+        return OUT_TICK
+    os.makedirs(os.path.dirname(OUT_TICK), exist_ok=True)
+    lib = os.path.dirname(OUT)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(REPO, "include"), src,
+                    "-L", lib, "-losc_controller", "-losc_batch", "-Wl,-rpath,$ORIGIN/../lib",
+                    "-Wl,-rpath-link,/opt/rocm/lib", "-o", OUT_TICK], check=True)
+    return OUT_TICK
 
 
 def build_controller(force: bool = False) -> str:

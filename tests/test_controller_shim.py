@@ -83,10 +83,11 @@ def test_gpu_kinematics_controller_arguments(robot):
     import torch
     out = run("gpu_lifecycle", robot)
     assert out["bad_state"] == INVALID_ARGUMENT           # State sized for another robot
-    assert out["init"] == OK and out["init_nt"] == OK
-    # a missing kinematic tree is a load failure (InternalError, as the XML load at osc.h:117);
-    # without a device the model creation fails first, also InternalError
-    assert out["opt_nt"] == INTERNAL
+    assert out["init"] == OK
+    # a missing kinematic tree fails initialize() with InternalError, as the reference's XML
+    # load does (osc.h:114-117); the optimization then has its precondition unmet (:164-165)
+    assert out["init_nt"] == INTERNAL
+    assert out["opt_nt"] == FAILED_PRECONDITION
 
 
 @pytest.mark.gpu

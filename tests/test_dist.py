@@ -48,3 +48,91 @@ def test_two_rank_gloo_bookkeeping(tmp_path):
         assert int(r[k]["total"]) == 8 + 12
         assert abs(float(r[k]["conv"]) - (8 + 11) / 20) < 1e-12
         assert abs(float(r[k]["value"]) - 20 * 10 / 2.0) < 1e-9
+
+
+# ---- bench.py's own per-rank path on two gloo ranks (the solve stubbed: no device here) ----
+
+class _StubSolver:
+    """Host stand-in for OSCBatchSolver with the calls bench.run_headline makes; every env
+    "converges" in 10 iterations.  Only the device work is stubbed: shards, timing, barriers and
+    the reduction are bench.py's own."""
+
+    def __init__(self, robot):
+        from osc_amd.robots import dims
+        self.robot = robot
+        self.nu = dims(robot)["nu"]
+
+    def prepare(self, M, C, J, b, T, mask):
+        return tuple(torch.from_numpy(x) for x in (M, C, J, b, T, mask))
+
+    def alloc_outputs(self, nenv):
+        import types
+        return types.SimpleNamespace(tau=torch.zeros(nenv, self.nu, dtype=torch.float64),
+                                     status=torch.zeros(nenv, dtype=torch.int32),
+                                     iters=torch.full((nenv,), 10, dtype=torch.int32))
+
+    def solve_into(self, out, *inputs):
+        out.tau.zero_()
+
+    def assemble_into(self, out, M, C, J, b, T, mask):
+        out.tau.copy_(M[:, :self.nu, 0])
+
+    def solve_assembled_into(self, out, mask):
+        out.status.zero_()
+
+
+def _bench_worker(rank, world, port, out_dir):
+    import json
+    import bench
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        args = bench.parse_args(["--gpus", str(world), "--steps", "3", "--warmup", "1",
+                                 "--nenv-per-gpu", "24", "--traffic-json", "/nonexistent"])
+        dev = torch.device("cpu")
+        line, _, inputs = bench.run_headline(args, world, rank, dev, lambda: barrier(world),
+                                             _StubSolver, bench.DeviceClock(dev))
+        np.save(os.path.join(out_dir, f"M{rank}.npy"), inputs[0].numpy())
+        if rank == 0:
+            with open(os.path.join(out_dir, "line.json"), "w") as fh:
+                json.dump(line, fh)
+        else:
+            assert line is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_path_two_gloo_ranks(tmp_path):
+    import json
+    world, port = 2, _free_port()
+    mp.spawn(_bench_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    line = json.load(open(tmp_path / "line.json"))
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["envs_per_gpu"] == 24
+    assert line["config"]["global_envs"] == 2 * 24
+    assert line["config"]["parallelism"] == "env-shard x2"
+    assert abs(line["value"] - 2 * 24 * 3 / (line["ms_per_step"] * 3 / 1e3)) <= 1e-6 * line["value"]
+    assert line["converged_frac"] == 1.0
+    # independent shards: each rank drew its own environments
+    assert not np.array_equal(np.load(tmp_path / "M0.npy"), np.load(tmp_path / "M1.npy"))
+
+
+def test_bench_launcher(monkeypatch):
+    """--gpus N > 1 without WORLD_SIZE: bench.py starts N ranks through torch.distributed.run on
+    127.0.0.1; WORLD_SIZE that disagrees with --gpus is refused."""
+    import subprocess
+    import bench
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.update(cmd=cmd, env=env) or 0)
+    argv = ["--gpus", "4", "--steps", "7"]
+    assert bench.launch_ranks(bench.parse_args(argv), argv) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert bench.launch_ranks(bench.parse_args(["--gpus", "1"]), ["--gpus", "1"]) is None
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.launch_ranks(bench.parse_args(["--gpus", "4"]), ["--gpus", "4"]) == 2
+    assert bench.launch_ranks(bench.parse_args(["--gpus", "2"]), ["--gpus", "2"]) is None
