@@ -143,6 +143,76 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
             "tick_from_joint_states_warm_mean_ipm_iters": float(out.iters.double().mean().item())}
 
 
+def tumbling_pipeline(solver, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
+    """BASELINE configs[3] as ONE device pipeline per control tick (SURVEY.md §8(f) rows 1 + 3):
+    joint states -> osc_batch_kinematics (M, C, J, b and the site positions) ->
+    osc_tumbling_targets (walter_sr_true_tumbling_mjjoint.cc:622-1019: shin angle / thigh height /
+    torso PD rows) -> osc_contact_mask_from_contacts (:473-558, a fresh synthetic contact list
+    per tick through the example's geom -> site rule) -> osc_batch_solve.  No host round trip
+    inside a tick.  The site positions stand in for the simulator's site_xpos the example reads.
+    Timed with HIP events on the launch stream; reported beside the headline, not as it."""
+    from osc_amd.kinematics import KinematicsBatch, load_tree, random_states
+    from osc_amd.producers import contact_geom_table, contact_mask_into, tumbling_targets_into
+    robot_tree = load_tree("walter_sr")
+    kb = KinematicsBatch(tree=robot_tree)
+    dev = solver.device
+    q0, v0 = random_states(robot_tree, nenv, seed, joint_range=0.5)
+    rng = np.random.default_rng(seed + 5)
+    nticks = 8
+    qs = [torch.from_numpy(q0 + 0.01 * (k + 1) * rng.standard_normal(q0.shape)).to(dev)
+          for k in range(nticks)]
+    for q in qs:
+        q[:, 3:7] = q[:, 3:7] / q[:, 3:7].norm(dim=1, keepdim=True)
+        q[:, 0:3] = 0.0
+    vs = [torch.from_numpy(v0 * (1 + 0.01 * rng.standard_normal(v0.shape))).to(dev)
+          for _ in range(nticks)]
+    q0d, v0d = torch.from_numpy(q0).to(dev), torch.from_numpy(v0).to(dev)
+    init = kb.compute(q0d, v0d, want_sites=True)               # the pre-loop snapshot (:363)
+    t0 = torch.zeros(nenv, dtype=torch.float64, device=dev)
+    ts = [torch.full((nenv,), 0.002 * (k + 1), dtype=torch.float64, device=dev)
+          for k in range(nticks)]
+    # contact lists: 20 geoms, geom g on body g, site s on body s: the example's id list marks
+    # contact site k for geom ids[k] (osc_contact_geom_table)
+    ids = (3, 4, 7, 8, 11, 12, 15, 16)
+    table = torch.from_numpy(contact_geom_table(np.arange(20), np.arange(17), ids)).to(dev)
+    max_con = 12
+    ncons = [torch.from_numpy(rng.integers(0, max_con + 1, nenv).astype(np.int32)).to(dev)
+             for _ in range(nticks)]
+    pairs = [torch.from_numpy(np.stack([np.zeros((nenv, max_con), np.int32),
+                                        rng.integers(0, 20, (nenv, max_con)).astype(np.int32)],
+                                       axis=2)).to(dev) for _ in range(nticks)]
+    kout = kb.alloc(nenv, want_sites=True)
+    T = torch.empty((nenv, 17, 6), dtype=torch.float64, device=dev)
+    mask = torch.empty((nenv, 8), dtype=torch.float64, device=dev)
+    out = solver.alloc_outputs(nenv)
+    k = [0]
+
+    def tick():
+        i = k[0] % nticks
+        kb.compute_into(kout, qs[i], vs[i])
+        tumbling_targets_into(T, qs[i], vs[i], kout.site_xpos, ts[i], t0, q0d, init.site_xpos)
+        contact_mask_into(mask, ncons[i], pairs[i], table)
+        solver.solve_into(out, kout.M, kout.C, kout.J, kout.b, T, mask)
+        k[0] += 1
+
+    for _ in range(warmup):
+        tick()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        tick()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return {"stages": "osc_batch_kinematics -> osc_tumbling_targets -> "
+                      "osc_contact_mask_from_contacts -> osc_batch_solve",
+            "envs": nenv, "tick_ms": ms, "solves_per_s": nenv / (ms * 1e-3),
+            "converged_frac": float((out.status == 0).double().mean().item()),
+            "mean_ipm_iters": float(out.iters.double().mean().item()),
+            "mean_contacts_active": float(mask.mean().item() * 8)}
+
+
 def run_mixed(args, world, rank, dev, barrier) -> None:
     """BASELINE configs[4]: mixed Go2 + WaLTER Sr.  Every rank solves its own shard of
     --nenv-per-gpu Go2 envs AND --nenv-per-gpu WaLTER envs (4,096 + 4,096 per GPU: 65,536 over 8
@@ -329,6 +399,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-single-env", action="store_true",
                     help="skip the configs[0] single-env tick latency reported beside the headline")
     ap.add_argument("--single-env-ticks", type=int, default=2000)
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="walter_sr tumbling: skip the whole-tick device pipeline timing")
     ap.add_argument("--mask-redraw", type=int, default=0,
                     help="cycle through this many Bernoulli masks, one per step (configs[3]: "
                          "contact-mode switching, walter_sr_true_tumbling_mjjoint.cc:554-614)")
@@ -525,6 +597,10 @@ def main(argv=None) -> None:
         if world == 1 and not args.no_front_end:   # rank-local extra; N=1 only, like cpu_baseline
             line["front_end"] = front_end(args.robot, solver, nenv, args.steps, args.warmup,
                                           shard_seed(rank), stream)
+        if world == 1 and args.robot == "walter_sr" and args.scenario == "tumbling" and \
+                not args.no_pipeline:
+            line["pipeline"] = tumbling_pipeline(solver, nenv, args.steps, args.warmup,
+                                                 shard_seed(rank) + 13, stream)
         if world == 1 and not args.no_single_env:
             line["single_env"] = single_env(args.robot, args.single_env_ticks)
         if world == 1 and not args.no_cpu:

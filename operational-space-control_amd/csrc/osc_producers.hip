@@ -7,8 +7,11 @@
 //                                               kp_a vec(q_ref q*) + kd_a (0 - w)], rows 1.. = 0
 //   osc_contact_mask_from_contacts
 //                            examples/walter_sr_true_tumbling_mjjoint.cc:473-558: a contact site's
-//                            mask is 1 iff some active contact of the env involves a geom that
-//                            belongs to that contact site's body (either side of the pair)
+//                            mask is 1 iff some active contact of the env involves a geom the
+//                            table maps to it (osc_contact_geom_table: the example's rule)
+//   osc_tumbling_targets     examples/walter_sr_true_tumbling_mjjoint.cc:622-1019: per-site PD
+//                            targets (shin angle, thigh height, torso) with the example's
+//                            finite differences against the initial snapshot
 //
 // Both are HBM-bound elementwise kernels: one thread per environment (PD) / per (env, contact)
 // (mask), grid-stride, 256-thread blocks.
@@ -75,6 +78,51 @@ __global__ __launch_bounds__(kBlock) void contact_mask_kernel(
   }
 }
 
+// Tumbling driver's per-site targets (walter_sr_true_tumbling_mjjoint.cc:622-1019), one thread
+// per environment.  Site rows: 0 torso, 1-4 shins, 5-8 thighs, 9-16 wheels (site_ids order).
+__global__ __launch_bounds__(kBlock) void tumbling_targets_kernel(
+    int nenv, int ns, int nq, int nv, const double* __restrict__ qpos,
+    const double* __restrict__ qvel, const double* __restrict__ site_xpos,
+    const double* __restrict__ tnow, const double* __restrict__ tstart,
+    const double* __restrict__ init_qpos, const double* __restrict__ init_site_xpos,
+    osc_tumbling_params P, double* __restrict__ T) {
+  for (int e = blockIdx.x * kBlock + threadIdx.x; e < nenv; e += gridDim.x * kBlock) {
+    const double* q = qpos + static_cast<size_t>(e) * nq;
+    const double* q0 = init_qpos + static_cast<size_t>(e) * nq;
+    const double* v = qvel + static_cast<size_t>(e) * nv;
+    const double* x = site_xpos + static_cast<size_t>(e) * ns * 3;
+    const double* x0 = init_site_xpos + static_cast<size_t>(e) * ns * 3;
+    const double t = tnow[e], dt = t - tstart[e];
+    double* o = T + static_cast<size_t>(e) * ns * 6;
+    for (int i = 0; i < 6 * ns; ++i) o[i] = 0.0;
+    // shins (:694-802): angular-y command from the shin joint angle
+    for (int i = 0; i < 4; ++i) {
+      const double th = q[P.shin_qadr[i]], th0 = q0[P.shin_qadr[i]];
+      const double w = (th - th0) / dt;
+      const double target = th0 + P.shin_rot_vel * t;
+      o[6 * (1 + i) + 4] = P.shin_kp * (target - th) + P.shin_kv * (P.shin_rot_vel - w);
+    }
+    // thighs (:866-973): linear-z command from the thigh site height
+    for (int i = 0; i < 4; ++i) {
+      const int r = 5 + i;
+      const double z = x[3 * r + 2], z0 = x0[3 * r + 2];
+      const double vz = (z - z0) / dt;
+      const double err = (z0 - 0.0 + P.thigh_height_offset) - z;
+      o[6 * r + 2] = P.thigh_lin_kp * err + P.thigh_lin_kv * (P.thigh_lin_vel - vz);
+    }
+    // torso (:981-1019): [lin_x, 0, 0, ang_x, ang_y, ang_z]
+    {
+      const double pe = (q0[0] + P.torso_lin_vel * t) - q[0];
+      const double ve = P.torso_lin_vel - v[0];
+      // rotation_error = vec(identity * conj(body_rotation)) = -(x, y, z) of (w, x, y, z)
+      const double re[3] = {-q[4], -q[5], -q[6]};
+      o[0] = P.torso_lin_kp * pe + P.torso_lin_kv * ve;
+      for (int k = 0; k < 3; ++k)
+        o[3 + k] = P.torso_ang_kp * re[k] + P.torso_ang_kv * (0.0 - v[3 + k]);
+    }
+  }
+}
+
 unsigned grid_for(long long n) {
   long long b = (n + kBlock - 1) / kBlock;
   if (b > 65535LL * 8) b = 65535LL * 8;
@@ -111,5 +159,64 @@ extern "C" int osc_contact_mask_from_contacts(int32_t nenv, int32_t nc, int32_t 
   hipLaunchKernelGGL(contact_mask_kernel, dim3(grid_for(static_cast<long long>(nenv) * nc)),
                      dim3(kBlock), 0, static_cast<hipStream_t>(stream), nenv, nc, max_con, ncon,
                      geom_pairs, ngeom, geom_to_site, contact_mask);
+  return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+
+extern "C" int osc_contact_geom_table(int32_t ngeom, const int32_t* geom_bodyid, int32_t nsite,
+                                      const int32_t* site_bodyid, int32_t nc, const int32_t* ids,
+                                      int32_t* geom_to_site) {
+  if (ngeom < 0 || nsite < 0 || nc < 0) return OSC_ERR_INVALID_ARGUMENT;
+  if (ngeom > 0 && (!geom_bodyid || !geom_to_site)) return OSC_ERR_INVALID_ARGUMENT;
+  if ((nsite > 0 && !site_bodyid) || (nc > 0 && !ids)) return OSC_ERR_INVALID_ARGUMENT;
+  for (int g = 0; g < ngeom; ++g) {
+    geom_to_site[g] = -1;
+    bool listed = false;   // role (1): the GEOM id is in the list (:526, :538)
+    for (int k = 0; k < nc; ++k) listed = listed || ids[k] == g;
+    if (!listed) continue;
+    int first = -1;        // getSiteIdsOnSameBodyAsGeom(g)[0] (:106-149, :529, :541)
+    for (int s = 0; s < nsite && first < 0; ++s)
+      if (site_bodyid[s] == geom_bodyid[g]) first = s;
+    if (first < 0) continue;
+    for (int k = 0; k < nc; ++k)   // role (2): the SITE id's position in the list (:152-163)
+      if (ids[k] == first) {
+        geom_to_site[g] = k;
+        break;
+      }
+  }
+  return OSC_OK;
+}
+
+extern "C" void osc_tumbling_params_default(osc_tumbling_params* p) {
+  if (!p) return;
+  p->shin_rot_vel = 0.1 * 8.0 * 5.0;
+  p->shin_kp = 800.0 * 3.0;
+  p->shin_kv = 800.0 * 3.0;
+  p->thigh_lin_vel = 0.0;
+  p->thigh_lin_kp = 4000.0 * 0.5;
+  p->thigh_lin_kv = 600.0 * 0.5;
+  p->thigh_height_offset = -0.025;
+  p->torso_lin_vel = 0.2;
+  p->torso_lin_kp = 0.0;
+  p->torso_lin_kv = 0.0;
+  p->torso_ang_kp = 0.0;
+  p->torso_ang_kv = 0.0;
+  const int32_t adr[4] = {8, 10, 12, 14};
+  for (int i = 0; i < 4; ++i) p->shin_qadr[i] = adr[i];
+}
+
+extern "C" int osc_tumbling_targets(int32_t nenv, int32_t ns, int32_t nq, int32_t nv,
+                                    const double* qpos, const double* qvel, const double* site_xpos,
+                                    const double* t, const double* t0, const double* init_qpos,
+                                    const double* init_site_xpos, const osc_tumbling_params* params,
+                                    double* targets, void* stream) {
+  if (nenv < 0 || ns != 17 || nq < 7 || nv < 6 || !params) return OSC_ERR_INVALID_ARGUMENT;
+  for (int i = 0; i < 4; ++i)
+    if (params->shin_qadr[i] < 7 || params->shin_qadr[i] >= nq) return OSC_ERR_INVALID_ARGUMENT;
+  if (nenv == 0) return OSC_OK;
+  if (!qpos || !qvel || !site_xpos || !t || !t0 || !init_qpos || !init_site_xpos || !targets)
+    return OSC_ERR_INVALID_ARGUMENT;
+  hipLaunchKernelGGL(tumbling_targets_kernel, dim3(grid_for(nenv)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), nenv, ns, nq, nv, qpos, qvel, site_xpos, t,
+                     t0, init_qpos, init_site_xpos, *params, targets);
   return hipGetLastError() == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
 }

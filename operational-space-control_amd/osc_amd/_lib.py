@@ -30,7 +30,9 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_qpos_workspace_bytes", "osc_batch_solve_qpos",
                     "osc_warm_state_bytes", "osc_batch_solve_warm", "osc_batch_solve_assembled_warm",
                     "osc_batch_solve_qpos_warm", "osc_batch_solve_multi",
-                    "osc_kin_desc_from_mjcf", "osc_kin_desc_from_mjcf_robot")
+                    "osc_kin_desc_from_mjcf", "osc_kin_desc_from_mjcf_robot",
+                    "osc_contact_geom_table", "osc_tumbling_params_default",
+                    "osc_tumbling_targets")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -52,6 +54,14 @@ class OscModelDesc(ctypes.Structure):
         ("eps_mu", ctypes.c_double),
         ("max_iter", ctypes.c_int32),
     ]
+
+
+class OscTumblingParams(ctypes.Structure):
+    """osc_tumbling_params (include/osc_producers.h)."""
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "shin_rot_vel", "shin_kp", "shin_kv", "thigh_lin_vel", "thigh_lin_kp", "thigh_lin_kv",
+        "thigh_height_offset", "torso_lin_vel", "torso_lin_kp", "torso_lin_kv", "torso_ang_kp",
+        "torso_ang_kv")] + [("shin_qadr", ctypes.c_int32 * 4)]
 
 
 class OscBatchJob(ctypes.Structure):
@@ -126,6 +136,14 @@ def lib() -> ctypes.CDLL:
     L.osc_pd_base_targets.restype = ctypes.c_int
     L.osc_contact_mask_from_contacts.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, vp]
     L.osc_contact_mask_from_contacts.restype = ctypes.c_int
+    ip32 = ctypes.POINTER(ctypes.c_int32)
+    L.osc_contact_geom_table.argtypes = [i32, ip32, i32, ip32, i32, ip32, ip32]
+    L.osc_contact_geom_table.restype = ctypes.c_int
+    L.osc_tumbling_params_default.argtypes = [ctypes.POINTER(OscTumblingParams)]
+    L.osc_tumbling_params_default.restype = None
+    L.osc_tumbling_targets.argtypes = [i32, i32, i32, i32] + [vp] * 7 + \
+        [ctypes.POINTER(OscTumblingParams), vp, vp]
+    L.osc_tumbling_targets.restype = ctypes.c_int
     L.osc_warm_state_bytes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t)]
     L.osc_warm_state_bytes.restype = ctypes.c_int
     L.osc_batch_solve_warm.argtypes = [vp, i32] + [vp] * 11 + [ctypes.c_size_t, vp,

@@ -20,7 +20,7 @@ def test_library_loads_and_exports_header_symbols():
     L = _lib.lib()
     declared = set()
     for h in HEADERS:
-        declared |= set(re.findall(r"^\s*(?:int|const char\*)\s+(osc_\w+)\s*\(", open(h).read(), re.M))
+        declared |= set(re.findall(r"^\s*(?:int|void|const char\*)\s+(osc_\w+)\s*\(", open(h).read(), re.M))
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name
