@@ -69,6 +69,8 @@ struct DevParams {
   int32_t warm_restart;              // warm start: re-centre an env still far off at this iteration
   int32_t restart_iter;              // cold start: the same, later
   int32_t max_iter;
+  int32_t refine_steps;              // full-space refinement steps after the interior point
+  double refine_penalty;             // active-row penalty, x max diag(Hr)
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -105,7 +107,16 @@ struct Dims {
   static constexpr int W_U = even(NY);
   static constexpr int W_HR = W_U + NUW * NY1P;
   static constexpr int W_X = W_HR + even(NY * NY);
-  static constexpr int WS = W_X + NXR * NY1P;
+  // torque coordinates: H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t), for the full-space
+  // refinement after the interior point (its gradient never goes through Hr)
+  static constexpr int W_HD = W_X + NXR * NY1P;
+  static constexpr int W_GD = W_HD + (TY ? NV * NV : 0);
+  // interior-point result handed to the refinement kernel: [y | q (lambda on rows with
+  // lambda > s, else 0; row slots) | status]
+  static constexpr int W_SOL = W_GD + (TY ? even(NV) : 0);
+  static constexpr int W_SQ = W_SOL + even(NY);
+  static constexpr int W_SST = W_SQ + NRL * 16;
+  static constexpr int WS = W_SOL + (TY ? even(NY) + NRL * 16 + 2 : 0);
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
   static constexpr int WW_Y = 2;
   static constexpr int WW_L = WW_Y + even(NY);
@@ -814,6 +825,10 @@ __device__ __forceinline__ void setup_env(
   for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
   for (int i = lane; i < D::NUW * NY1P; i += kWave) w[D::W_U + i] = sU[i];
   for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
+  if constexpr (D::TY) {
+    for (int i = lane; i < NV * NV; i += kWave) w[D::W_HD + i] = sHa[(i / NV) * NA + i % NV];
+    for (int i = lane; i < NV; i += kWave) w[D::W_GD + i] = sHa[i * NA + NV];
+  }
   STAMP_END(5);
   STAMP_STORE_SETUP();
 }
@@ -991,9 +1006,19 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
 // its registers would allow two, the LDS request (> 160 KB / 5 per workgroup) is what keeps the
 // dispatcher from stacking a fifth and sixth workgroup on some CUs while others idle (Go2 in
 // torque coordinates: 26 KB of LDS, 255 VGPRs -> IPM 144 -> 158 us at 4,096 envs until padded).
-template <class D, bool SMALL>
+// The refinement pass (REFINE) streams Hr from L2 and keeps instead each env's [X | H_dv | f_dv]
+// block of the workspace in LDS (RefineLds).
+template <class D>
+struct RefineLds {
+  static constexpr int X = 0;
+  static constexpr int HD = D::NV * D::NY1P;
+  static constexpr int GD = HD + D::NV * D::NV;
+  static constexpr int SIZE = GD + even(D::NV);   // = W_SOL - W_X in the workspace
+};
+template <class D, bool SMALL, bool REFINE = false>
 constexpr int ipm_lds_doubles() {
-  constexpr int il = IpmLayout<D, SMALL && hr_fits_lds<D>()>::IL;
+  constexpr int il = IpmLayout<D, SMALL && !REFINE && hr_fits_lds<D>()>::IL +
+                     (REFINE ? RefineLds<D>::SIZE : 0);
   return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
 }
 
@@ -1001,7 +1026,7 @@ constexpr int ipm_lds_doubles() {
 // doubles of LDS.  Wrapped by osc_ipm_kernel (one model) and osc_ipm_pair_kernel (two models).
 // WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
 // is unchanged by it: the two-wave Go2 variant would otherwise spill more).
-template <class D, bool SMALL, bool WARM>
+template <class D, bool SMALL, bool WARM, bool REFINE = false>
 __device__ __forceinline__ void ipm_block(
     const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
@@ -1009,8 +1034,9 @@ __device__ __forceinline__ void ipm_block(
     int fixup, double* __restrict__ sm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
-  constexpr bool HRL = SMALL && hr_fits_lds<D>();
+  constexpr bool HRL = SMALL && !REFINE && hr_fits_lds<D>();
   using LY = IpmLayout<D, HRL>;
+  if constexpr (REFINE && !D::TY) return;   // refinement exists in torque coordinates only
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
   const int env_raw = blk * kEnvPerWave + grp;
@@ -1025,7 +1051,9 @@ __device__ __forceinline__ void ipm_block(
     write_out = valid && (!fixup || redo);
   }
 
-  double* B = sm + grp * LY::IL;
+  constexpr int kEnvLds = LY::IL + (REFINE ? RefineLds<D>::SIZE : 0);
+  double* B = sm + grp * kEnvLds;
+  double* sRef = B + LY::IL;   // REFINE: [X | H_dv | f_dv] of this env
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -1351,6 +1379,30 @@ __device__ __forceinline__ void ipm_block(
     any_warm = __ballot(warm) != 0;
     all_warm = __ballot(!warm) == 0;
   }
+  if constexpr (REFINE) {
+    // the interior point's result for this env (osc_ipm_kernel, W_SOL): y, and the active rows
+    // as lambda > s with lambda = q > 0
+    static_assert(D::W_SOL - D::W_X == RefineLds<D>::SIZE && D::W_X % 2 == 0 &&
+                  RefineLds<D>::SIZE % 2 == 0, "refinement LDS block = workspace [X | H_dv | f_dv]");
+    {
+      Batch2<RefineLds<D>::SIZE / 2, kRow> bx;
+      bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X, l);
+      bx.store(sRef, l);
+    }
+    const double* sol = ws + static_cast<size_t>(env) * D::WS + D::W_SOL;
+    y0 = sol[j0];
+    y1 = v1 ? sol[j1] : 0.0;
+#pragma unroll
+    for (int t = 0; t < NRL; ++t) {
+      const double q = sol[even(NY) + l + kRow * t];
+      lam[t] = q;
+      s[t] = q > 0.0 ? 0.0 : 1.0;
+    }
+    st = static_cast<int32_t>(sol[even(NY) + NRL * kRow]);
+    sVy[j0] = y0;
+    if (v1) sVy[j1] = y1;
+    wave_sync();
+  } else
   for (int it = all_warm ? 0 : -1;; ++it) {
     STAMP_BEGIN();
     const bool init = it < 0;
@@ -1634,8 +1686,197 @@ __device__ __forceinline__ void ipm_block(
     STAMP_END(7);
   }
   STAMP_STORE();
+  if constexpr (D::TY && !REFINE) {   // hand the result to the refinement kernel
+    if (write_out) {
+      // (the W_SOL block is written here and read by nothing else in this kernel)
+      double* sol = const_cast<double*>(ws) + static_cast<size_t>(env) * D::WS + D::W_SOL;
+      sol[j0] = y0;
+      if (v1) sol[j1] = y1;
+#pragma unroll
+      for (int t = 0; t < NRL; ++t)
+        sol[even(NY) + l + kRow * t] = (act[t] && lam[t] > s[t]) ? lam[t] : 0.0;
+      if (l == 0) sol[even(NY) + NRL * kRow] = static_cast<double>(st);
+    }
+  }
+
+  // ---------------- full-space refinement (torque coordinates) ---------------
+  // Hr is an explicitly formed fp64 product X'H_dv X whose condition number reaches ~1e10, so the
+  // interior point's optimum of the reduced QP sits up to ~1e-5 (normwise) off the optimum of
+  // the QP the reference defines.  Iterative refinement on the active set of the converged
+  // iterate (rows with lambda > s) removes that: the residual is formed in factored form,
+  //   r = X_y' (H_dv (X [y;1]) + f_dv) + 2 (w_tau + w_reg) u + 2 w_reg z + G_A' mu,
+  // which never goes through Hr, and the correction comes from one LDL^T of
+  // K_A = Hr + D G_A'G_A (active rows by penalty D = refine_penalty x max diag Hr; dependent rows
+  // of a contact at the pyramid apex are harmless there):
+  //   K_A dy = -r - D G_A'(G_A y - h_A),   mu += D (G_A (y + dy) - h_A),   y += dy.
+  // Two steps take the worst envs of 32,768-env batches from 7e-6 to ~1e-13 of the exact optimum
+  // (tools/ipm_model.py + the refinement study in DESIGN.md).  Envs that did not converge keep
+  // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
+  // discarded.
+  bool refined = false;
+  if constexpr (D::TY && REFINE) {
+    const bool mine = valid && st == OSC_SOLVE_OK;
+    if (P->refine_steps > 0 && __ballot(mine) != 0) {
+      const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
+      const double ytol = 1e-9 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)));
+      double Dr[NRL], mur[NRL];
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        const bool a = act[t] && lam[t] > s[t];
+        Dr[t] = a ? dpen : 0.0;
+        mur[t] = a ? lam[t] : 0.0;
+      }
+      const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg;
+      double ya0 = y0, ya1 = y1;
+      bool viol_env = false;
+      // rounds: a row the refined point violates was active at the optimum with a vanishing
+      // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
+      // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
+      for (int round = 0; round < 3; ++round) {
+        if (round > 0) {
+          load_hr();   // c0 / c1 hold the last round's factor
+        }
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) sDr[l + kRow * t] = Dr[t];
+        ya0 = y0;
+        ya1 = y1;
+        sVy[j0] = y0;
+        if (v1) sVy[j1] = y1;
+        wave_sync();
+        // K_A in c0 / c1 (they hold Hr's columns)
+        double dg0 = hdg0, dg1 = hdg1;
+        {
+          const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
+          const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
+          dg0 += du;
+          static_for<0, NU>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            c0[i] += keep_lanes<rows_mask(1u << i)>(du);
+          });
+        }
+        if (jk0 >= 0) {
+          double a, b, cc;
+          contact_col(jk0, jc0, a, b, cc);
+          dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
+#pragma unroll
+          for (int i = NU; i < NY; ++i) {
+            const int ki = (i - NU) / 3, ci = (i - NU) % 3;
+            c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
+          }
+        }
+        if (jk1 >= 0) {
+          double a, b, cc;
+          contact_col(jk1, jc1, a, b, cc);
+          dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
+#pragma unroll
+          for (int i = NU; i < NY; ++i) {
+            const int ki = (i - NU) / 3, ci = (i - NU) % 3;
+            c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
+          }
+        }
+        wave_sync();
+        ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+        wave_sync();
+        for (int k = 0; k < P->refine_steps; ++k) {
+          // dv = X [y; 1] (rows l, l + 16) -> sXb
+#pragma unroll
+          for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
+            const int rr = l + kRow * t;
+            if (rr < NV) {
+              const double* xr = sRef + RefineLds<D>::X + rr * NY1P;
+              double a = xr[NY];
+#pragma unroll
+              for (int i = 0; i < NY; ++i) a = fma(xr[i], sVy[i], a);
+              sXb[rr] = a;
+            }
+          }
+          wave_sync();
+          // gx = H_dv dv + f_dv (rows l, l + 16) -> sDr[0 .. NV)
+          double gxr[(NV + kRow - 1) / kRow];
+#pragma unroll
+          for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
+            const int rr = l + kRow * t;
+            gxr[t] = 0.0;
+            if (rr < NV) {
+              const double* hr = sRef + RefineLds<D>::HD + rr * NV;
+              double a = sRef[RefineLds<D>::GD + rr];
+#pragma unroll
+              for (int i = 0; i < NV; ++i) a = fma(hr[i], sXb[i], a);
+              gxr[t] = a;
+            }
+          }
+          wave_sync();
+#pragma unroll
+          for (int t = 0; t < (NV + kRow - 1) / kRow; ++t)
+            if (l + kRow * t < NV) sDr[l + kRow * t] = gxr[t];
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) sVr[l + kRow * t] = mur[t];
+          wave_sync();
+          // r_j = X[:, j]' gx + diag_j y_j + (G_A' mu)_j for the lane's two variables
+          double r0 = (j0 < NU ? wu : wz) * ya0, r1 = (jj1 < NU ? wu : wz) * ya1;
+#pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            r0 = fma(sRef[RefineLds<D>::X + i * NY1P + j0], sDr[i], r0);
+            r1 = fma(sRef[RefineLds<D>::X + i * NY1P + jj1], sDr[i], r1);
+          }
+          double gm0, gm1;
+          GTw2(sVr, gm0, gm1);
+          r0 += gm0;
+          r1 += gm1;
+          wave_sync();
+          double R3[NRL];
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) {
+            R3[t] = (Dr[t] != 0.0) ? Gv(sVy, t) - h[t] : 0.0;
+            sVr[l + kRow * t] = Dr[t] * R3[t];
+          }
+          wave_sync();
+          double b0, b1;
+          GTw2(sVr, b0, b1);
+          double d0 = -r0 - b0, d1 = -r1 - b1;
+          ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, d0, d1, l);
+          sVy2[j0] = d0;
+          if (v1) sVy2[j1] = d1;
+          wave_sync();
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) mur[t] += Dr[t] * (Gv(sVy2, t) + R3[t]);
+          ya0 += d0;
+          ya1 += d1;
+          wave_sync();
+          sVy[j0] = ya0;
+          if (v1) sVy[j1] = ya1;
+          wave_sync();
+        }
+        // rows the refined point violates join the active set
+        double nviol = 0.0;
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          const bool v = act[t] && Dr[t] == 0.0 && Gv(sVy, t) - h[t] > ytol;
+          Dr[t] = v ? dpen : Dr[t];
+          nviol += v ? 1.0 : 0.0;
+        }
+        viol_env = mine && row_max(nviol) > 0.0;
+        if (__ballot(viol_env) == 0) break;
+      }
+      // keep the refined iterate when it is feasible, finite and close to the interior point's
+      const double mv = fmax(fabs(ya0 - y0), v1 ? fabs(ya1 - y1) : 0.0);
+      const double my = fmax(fabs(y0), v1 ? fabs(y1) : 0.0);
+      const double ok = (isfinite(ya0) && isfinite(ya1) && mv <= 1e-3 * (1.0 + my)) ? 1.0 : 0.0;
+      const bool keep = !viol_env && row_min(ok) == 1.0;
+      if (mine && keep) {
+        y0 = ya0;
+        y1 = ya1;
+        refined = true;
+      }
+      wave_sync();
+      sVy[j0] = y0;
+      if (v1) sVy[j1] = y1;
+      wave_sync();
+    }
+  }
 
   // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
+  if (REFINE && !refined) write_out = false;   // the interior point's outputs stand
   if (l < NU) {
     double tq = D::TY ? sVy[l] : sU[l * NY1P + NY];
 #pragma unroll
@@ -1674,11 +1915,11 @@ __device__ __forceinline__ void ipm_block(
         }
       }
     }
-    if (l == 0) {
+    if (l == 0 && !REFINE) {
       if (gstatus) gstatus[env] = st;
       if (giters) giters[env] = (WARM && fixup) ? P->max_iter + it_done : it_done;   // both passes
     }
-    if (WARM) {   // this tick's y and lambda for the next one (NaN: next tick cold)
+    if (WARM && !REFINE) {   // this tick's y and lambda for the next one (NaN: next tick cold)
       double* wo = gwarm + static_cast<size_t>(env) * D::WW;
       wo[D::WW_Y + j0] = y0;
       if (v1) wo[D::WW_Y + j1] = y1;
@@ -1690,15 +1931,27 @@ __device__ __forceinline__ void ipm_block(
   }
 }
 
-template <class D, bool SMALL, bool WARM>
+template <class D, bool SMALL, bool WARM, bool REFINE = false>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
     int fixup) {
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL>()];
-  ipm_block<D, SMALL, WARM>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx, gstatus,
-                            giters, gwarm, fixup, sm);
+  ipm_block<D, SMALL, WARM, REFINE>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
+                                    gstatus, giters, gwarm, fixup, sm);
+}
+
+// The full-space refinement pass (torque coordinates): the same body with the interior-point
+// loop compiled out, started from the result the interior point left in W_SOL, so its extra
+// state never weighs on the interior point's register allocation.
+template <class D, bool SMALL>
+__global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_refine_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx) {
+  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, true>()];
+  ipm_block<D, SMALL, false, true>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
+                                   nullptr, nullptr, nullptr, 0, sm);
 }
 
 // Two models' interior point in one grid, one wavefront per SIMD (the one-wave variant of both):
@@ -1706,23 +1959,23 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 // in order, so with the slower model first the faster model's wavefronts fill the SIMDs that
 // the first model's early finishers free (its iteration-count tail) -- two grids on two streams
 // instead split the SIMDs between the models and each pays its own tail.
-template <class DA, class DB>
+template <class DA, class DB, bool REFINE = false>
 __global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, PairArgs B) {
-  __shared__ __attribute__((aligned(16)))
-      double sm[cmax(ipm_lds_doubles<DA, true>(), ipm_lds_doubles<DB, true>())];
+  __shared__ __attribute__((aligned(16))) double
+      sm[cmax(ipm_lds_doubles<DA, true, REFINE>(), ipm_lds_doubles<DB, true, REFINE>())];
   const int nbA = (A.nenv + kEnvPerWave - 1) / kEnvPerWave;
   const int blk = static_cast<int>(blockIdx.x);
   if (blk < nbA)
-    ipm_block<DA, true, false>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status, A.iters,
-                               nullptr, 0, sm);
+    ipm_block<DA, true, false, REFINE>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status,
+                                       A.iters, nullptr, 0, sm);
   else
-    ipm_block<DB, true, false>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x, B.status,
-                               B.iters, nullptr, 0, sm);
+    ipm_block<DB, true, false, REFINE>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x,
+                                       B.status, B.iters, nullptr, 0, sm);
 }
 
 using Go2 = Dims<18, 12, 4, 5, true>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites; y = (u, z)
 #ifndef OSC_WALTER_TY
-#define OSC_WALTER_TY 0
+#define OSC_WALTER_TY 1
 #endif
 using Walter = Dims<14, 8, 8, 17, OSC_WALTER_TY>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
 
@@ -1759,6 +2012,7 @@ struct osc_model {
   DevParams* dparams;
   int device;
   int small_batch_max;   // envs that fit one wavefront per SIMD (4 per wave x 4 SIMDs x CUs)
+  bool refine;           // torque-coordinate model with refinement steps > 0
 };
 
 extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
@@ -1809,6 +2063,12 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.warm_center = 0.3;
   hp.warm_restart = 22;
   hp.restart_iter = 28;
+  // full-space refinement: two steps with one factorisation, penalty 1e2 x the
+  // largest reduced-Hessian diagonal (numpy model: <= 3e-12 normwise on Go2 / WaLTER batches,
+  // from up to 7e-6 without it)
+  hp.refine_steps = 2;
+  hp.refine_penalty = 1e2;
+  if (const char* e = std::getenv("OSC_REFINE_STEPS")) hp.refine_steps = std::atoi(e);
   if (const char* e = std::getenv("OSC_RESTART_ITER")) hp.restart_iter = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);
@@ -1819,6 +2079,8 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   m->desc = d;
   m->kid = kid;
   m->dparams = nullptr;
+  m->refine = hp.refine_steps > 0 &&
+              ((kid == K_GO2 && Go2::TY) || (kid == K_WALTER && Walter::TY));
   (void)hipGetDevice(&m->device);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess)
@@ -1906,6 +2168,14 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
           hipLaunchKernelGGL((osc_ipm_kernel<D, false, true>), dim3(nb), dim3(kWave), 0, s,
                              model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
       }
+    }
+    if (D::TY && model->refine) {
+      if (small)
+        hipLaunchKernelGGL((osc_refine_kernel<D, true>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x);
+      else
+        hipLaunchKernelGGL((osc_refine_kernel<D, false>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x);
     }
   }
 }
@@ -1995,6 +2265,8 @@ void launch_pair(const osc_batch_job& a, const osc_batch_job& b, hipStream_t s) 
   const unsigned nb = static_cast<unsigned>((a.nenv + kEnvPerWave - 1) / kEnvPerWave +
                                             (b.nenv + kEnvPerWave - 1) / kEnvPerWave);
   hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB>), dim3(nb), dim3(kWave), 0, s, A, B);
+  if (a.model->refine || b.model->refine)
+    hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB, true>), dim3(nb), dim3(kWave), 0, s, A, B);
 }
 
 }  // namespace

@@ -103,6 +103,20 @@ def kkt_certificate(qp: QPData, x: np.ndarray, y: np.ndarray) -> dict:
                 complementarity=float(comp / (scale_d * scale_p)))
 
 
+def _kkt_solve(K, rhs):
+    """The working-set KKT system.  When the working set is linearly dependent -- a contact at
+    the pyramid apex, where its four pyramid rows and fz >= 0 are all active on three forces --
+    K is exactly singular: x is still unique (H > 0), the multipliers are not; least squares
+    returns x and the minimum-norm multipliers."""
+    try:
+        sol = np.linalg.solve(K, rhs)
+        if np.all(np.isfinite(sol)):
+            return sol
+    except np.linalg.LinAlgError:
+        pass
+    return np.linalg.lstsq(K, rhs, rcond=None)[0]
+
+
 def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
                 refine_steps: int = 4) -> ExactSolution:
     n = model.n
@@ -125,7 +139,7 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
         K[:n, :n] = qp.H
         K[:n, n:] = rows.T
         K[n:, :n] = rows
-        sol = np.linalg.solve(K, np.concatenate([-qp.f, rhs_b]))
+        sol = _kkt_solve(K, np.concatenate([-qp.f, rhs_b]))
         p, lam = sol[:n] - x, sol[n:]
         if np.abs(p).max() <= 1e-9 * (1.0 + np.abs(x).max()):
             x = sol[:n]
@@ -158,7 +172,7 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
     K[:n, n:] = rows.T
     K[n:, :n] = rows
     rhs = np.concatenate([-qp.f, rhs_b])
-    sol = np.linalg.solve(K, rhs)
+    sol = _kkt_solve(K, rhs)
     # Mixed-precision iterative refinement: residuals in x87 extended precision (eps ~1e-19),
     # corrections from the fp64 factorisation.  Converges to ~eps_ext * cond(K), i.e. well
     # below fp64 round-off for this QP (cond(K) ~ 1e8..1e10 with w_reg = 1e-4).
@@ -167,7 +181,7 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
     soll = sol.astype(np.longdouble)
     for _ in range(refine_steps):
         r = rhsl - Kl @ soll
-        soll = soll + np.linalg.solve(K, r.astype(np.float64)).astype(np.longdouble)
+        soll = soll + _kkt_solve(K, r.astype(np.float64)).astype(np.longdouble)
     sol = soll.astype(np.float64)
     x, lam = sol[:n], sol[n:]
     y = np.zeros(A.shape[0])

@@ -41,14 +41,18 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     sz = nbytes.value // 8 // nenv
     ev = lambda a: (a + 1) // 2 * 2
     ny1p = ev(ny + 1)
-    # layout documented in include/osc_batch.h: [g | U | Hr | X], or [g | Hr | X] with nv rows
-    # of X in torque coordinates
+    # layout documented in include/osc_batch.h: torque coordinates (both robots by default,
+    # Dims<..., TY = true> in csrc/osc_batch.hip): [g | Hr | X (nv rows) | H_dv | f_dv | sol]
+    # (sol = the interior point's y / active multipliers / status for the refinement pass)
     o_g, o_u = 0, ev(ny)
-    ty = robot == "unitree_go2"                 # Dims<..., TY = true> in csrc/osc_batch.hip
+    ty = True
     nxr = nv if ty else nb
     o_hr = o_u + (0 if ty else nu * ny1p)
     o_x = o_hr + ev(ny * ny)
-    assert sz == o_x + nxr * ny1p
+    o_hd = o_x + nxr * ny1p
+    o_gd = o_hd + nv * nv
+    nrl = (2 * nu + 6 * nc + 15) // 16
+    assert sz == o_gd + ev(nv) + ev(ny) + nrl * 16 + 2
     dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     rc = L.osc_batch_assemble(s._h, nenv, *[p(a) for a in args], p(dbg), nbytes,
@@ -62,7 +66,13 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
         Hr = D[e, o_hr:o_hr + ny * ny].reshape(ny, ny)
         g = D[e, o_g:o_g + ny]
         U = np.eye(nu, ny + 1) if ty else D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
-        X = D[e, o_x:].reshape(nxr, ny1p)[:, :ny + 1]
+        X = D[e, o_x:o_hd].reshape(nxr, ny1p)[:, :ny + 1]
+        # H_dv / f_dv: the dv blocks of the oracle's H and f (autogen.py:304-319)
+        a_ = [inp[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        qp_ = build_qp(model, *a_)
+        Hd, gd = D[e, o_hd:o_gd].reshape(nv, nv), D[e, o_gd:o_gd + nv]
+        assert np.abs(Hd - qp_.H[:nv, :nv]).max() <= 1e-12 * np.abs(qp_.H[:nv, :nv]).max()
+        assert np.abs(gd - qp_.f[:nv]).max() <= 1e-12 * max(np.abs(qp_.f[:nv]).max(), 1.0)
         np.testing.assert_array_equal(Hr, Hr.T)
         a = [inp[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a)

@@ -149,3 +149,27 @@ def test_reference_port_default_settings_converge():
         assert 0 < it < 4000
         ref = g["tau"][e]
         assert np.abs(tau - ref).max() / max(np.abs(ref).max(), 1.0) < 0.2
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])
+def test_closed_form_equals_literal_autogen_objective(robot):
+    """build_qp's H and f against the objective written term by named term as autogen.py writes
+    it (oracle/autogen_literal.py), with the reference's own weights file when it is present:
+    the literal objective is a quadratic, so its Hessian and gradient at x = 0 follow exactly
+    from values at 0, +-e_i and e_i + e_j."""
+    import autogen_literal as lit
+    from osc_amd.robots import config_path
+    from osc_amd.synth import SEED_BASE, generate
+    ref_yaml = os.path.join("/root/reference/config", robot, f"{robot}_config.yaml")
+    yaml_path = ref_yaml if os.path.exists(ref_yaml) else config_path(robot)
+    weights = lit.weights_config(yaml_path)
+    model = load_model(robot)
+    d = generate(robot, 2, SEED_BASE + 61, "tumbling", "bernoulli")
+    for e in range(2):
+        M, C, J, b, T, mask = (d[k][e] for k in ("M", "C", "J", "b", "T", "mask"))
+        qp = build_qp(model, M, C, J, b, T, mask)
+        H, g = lit.hessian_gradient_at_zero(
+            lambda x: lit.objective(robot, weights, x, T, J, b, model.nv, model.nu), model.n)
+        scale = np.abs(qp.H).max()
+        assert np.abs(H - qp.H).max() <= 1e-9 * scale, np.abs(H - qp.H).max() / scale
+        assert np.abs(g - qp.f).max() <= 1e-9 * max(np.abs(qp.f).max(), 1.0)

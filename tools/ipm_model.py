@@ -124,6 +124,9 @@ def ldl_solve(F, r):
     return sla.solve_triangular(L.T, z / d, lower=False, unit_diagonal=True)
 
 
+FINAL = {}     # (s, lam) of the last returned iterate, for refinement studies
+RD_EXACT = None   # optional y -> Hr y + g evaluated in factored form (X'(Hdv (X y + x0) + gdv) ..)
+RD_EXACT_MU = 1e-6
 NU_STOP = 12   # torque entries of y in torque coordinates (Go2) for the "ustop" variant
 TRACE = None   # set to a list to record (it, mu, a_aff, a, alpha, sigma) per iteration
 
@@ -196,8 +199,11 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
                 rp_c = rp
             rp = rp_c
         rd = Hr @ y + g + G.T @ lam
+        if RD_EXACT is not None and s @ lam / m <= RD_EXACT_MU:
+            rd = RD_EXACT(y) + G.T @ lam     # factored gradient (never through Hr)
         mu = s @ lam / m
         if mu <= eps_mu:
+            FINAL.update(s=s.copy(), lam=lam.copy())
             return y, it, True
         ustop = [v for v in variant if v.startswith("ustop")]
         if ustop and last_du is not None:
@@ -207,6 +213,7 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
             if mu <= mth and last_du <= tol * max(np.abs(y[:NU_STOP]).max(), 1.0):
                 return y, it, True
         if it >= max_iter:
+            FINAL.update(s=s.copy(), lam=lam.copy())
             return y, it, False
         pol = [float(v[6:]) for v in variant if v.startswith("polish")]
         if pol and mu <= pol[0]:
