@@ -2069,6 +2069,7 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.refine_steps = 2;
   hp.refine_penalty = 1e2;
   if (const char* e = std::getenv("OSC_REFINE_STEPS")) hp.refine_steps = std::atoi(e);
+  if (const char* e = std::getenv("OSC_EPS_MU")) hp.eps_mu = std::atof(e);   // sweeps only
   if (const char* e = std::getenv("OSC_RESTART_ITER")) hp.restart_iter = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);

@@ -1,12 +1,16 @@
 """GPU parity tests: the HIP path (through the C-ABI) against the exact CPU oracle.
 
 Tolerance (stated, per BASELINE.md "torques within 1e-5 rel of the CPU reference"):
-  * normwise:    max_i |tau_i - tau*_i| / max(||tau*||_inf, 1)          <= 1e-5
-  * elementwise: |tau_i - tau*_i| / max(|tau*_i|, 1e-2 ||tau*||_inf)    <= 1e-4
-where tau* is the oracle's certified exact optimum.  The QP has regularisation-only directions
-(curvature 2 w_reg = 2e-4: internal contact forces), so tiny torques are relatively less
-determined; the normwise bound is the contract, the elementwise one a guard.
-Measured on the goldens the HIP path sits around 1e-7 normwise.
+  * contract, normwise:  max_i |tau_i - tau*_i| / max(||tau*||_inf, 1)                  <= 1e-5
+  * contract, elementwise, every torque above 1 % of the norm:
+                         |tau_i - tau*_i| / |tau*_i|  for |tau*_i| >= 1e-2 ||tau*||_inf   <= 1e-5
+  * achieved (the full-space refinement after the interior point):
+                         normwise <= 1e-9, elementwise above the floor <= 1e-7
+where tau* is the oracle's certified exact optimum.  Below the 1 % floor a torque is only
+weakly determined by the QP itself (regularisation-only curvature 2 w_reg = 2e-4: internal
+contact forces); the normwise bound covers it.  Measured (tools/hardest_envs.py on every env of
+32,768-env tumbling batches): worst normwise 1.2e-11 (Go2) / 2.2e-11 (WaLTER), worst
+elementwise above the floor 3.7e-11 / 1.6e-10.
 """
 import glob
 import os
@@ -24,8 +28,10 @@ from qp_exact import solve_exact
 pytestmark = pytest.mark.gpu
 
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
-NORM_TOL = 1e-5
-ELEM_TOL = 1e-4
+NORM_TOL = 1e-5          # contract
+ELEM_TOL = 1e-5          # contract, above the 1 % floor
+NORM_ACH = 1e-9          # achieved with the refinement
+ELEM_ACH = 1e-7
 
 _solvers = {}
 
@@ -38,11 +44,19 @@ def solver(robot):
 
 
 def _rel_errors(tau, ref):
+    """(normwise, elementwise over the torques at or above 1 % of the env's norm)."""
     tau, ref = np.asarray(tau), np.asarray(ref)
     nrm = np.maximum(np.abs(ref).max(axis=-1, keepdims=True), 1.0)
     normwise = (np.abs(tau - ref) / nrm).max(axis=-1)
-    elem = (np.abs(tau - ref) / np.maximum(np.abs(ref), 1e-2 * nrm)).max(axis=-1)
+    big = np.abs(ref) >= 1e-2 * np.abs(ref).max(axis=-1, keepdims=True)
+    elem = np.where(big, np.abs(tau - ref) / np.maximum(np.abs(ref), 1e-300), 0.0).max(axis=-1)
     return normwise, elem
+
+
+def _check(nw, el, where=""):
+    assert nw.max() <= NORM_TOL and el.max() <= ELEM_TOL, (where, nw.max(), el.max())
+    assert nw.max() <= NORM_ACH, (where, "normwise", nw.max(), int(np.argmax(nw)))
+    assert el.max() <= ELEM_ACH, (where, "elementwise", el.max(), int(np.argmax(el)))
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
@@ -53,11 +67,10 @@ def test_golden_torques(gpu, path):
     torch.cuda.synchronize()
     assert (res.status.cpu().numpy() == 0).all(), res.status
     nw, el = _rel_errors(res.tau.cpu().numpy(), g["tau"])
-    assert nw.max() <= NORM_TOL, nw
-    assert el.max() <= ELEM_TOL, el
+    _check(nw, el, os.path.basename(path))
     x = res.x.cpu().numpy()
     nx = (np.abs(x - g["x"]) / np.maximum(np.abs(g["x"]).max(axis=1, keepdims=True), 1.0)).max()
-    assert nx <= NORM_TOL, nx
+    assert nx <= NORM_ACH, nx
     # masked contacts: forces exactly zero (bounds l = u = 0, osc.h:492-495)
     model = load_model(robot)
     z = x[:, model.nv + model.nu:].reshape(x.shape[0], model.nc, 3)
@@ -84,27 +97,37 @@ def test_fresh_batch_vs_oracle(gpu, robot, scenario, mask_mode, seed):
         ref.append(torque(model, solve_exact(model, build_qp(model, *args), *args[:3]).x))
     nw, el = _rel_errors(res.tau.cpu().numpy(), np.array(ref))
     assert (res.status.cpu().numpy() == 0).all()
-    assert nw.max() <= NORM_TOL, (nw.max(), np.argmax(nw))
-    assert el.max() <= ELEM_TOL, (el.max(), np.argmax(el))
+    _check(nw, el, robot)
 
 
-def test_go2_hardest_envs_vs_oracle(gpu):
-    """The Go2 environments of a 32,768-env tumbling batch whose torques moved most when Go2
-    switched to torque coordinates y = (u, z): the (dv_a, z) form missed the
-    optimum by up to 4.3e-5 normwise on them, the torque form is within 5e-7.  Solved as part of
-    the full batch (lockstep partners and all), checked against the exact oracle."""
-    d = generate("unitree_go2", 32768, SEED_BASE + 7, "tumbling", "bernoulli")
-    res = solver("unitree_go2").solve(**d)
+# Environments of the 32,768-env tumbling batches (seed SEED_BASE + 7) that were hardest for
+# some version of the solver (tools/dump_tau.py + tools/hardest_envs.py over every env):
+#   Go2: 22286 (6.9e-6 normwise / 2e-4 elementwise before the refinement), 13178, 5364 (the
+#        next worst), 17721 (worst after it), 1092, 23275, 26327, 2028, 22513 (worst of the
+#        (dv_a, z) coordinates);
+#   WaLTER: 3034, 30946, 7962, 4701 (a degenerate contact row misread as inactive by the
+#        first refinement -- 2e-4 before violated rows joined the active set), 10371, 943,
+#        24601 (worst of the (dv_a, z) interior point), 10968, 31298 (worst now).
+HARDEST = {"unitree_go2": [22286, 13178, 5364, 17721, 1092, 23275, 26327, 2028, 22513],
+           "walter_sr": [3034, 30946, 7962, 4701, 10371, 943, 24601, 10968, 31298]}
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
+def test_hardest_envs_vs_oracle(gpu, robot):
+    """Solved as part of the full 32,768-env batch (lockstep partners and all), checked against
+    the exact oracle at the achieved tolerance."""
+    d = generate(robot, 32768, SEED_BASE + 7, "tumbling", "bernoulli")
+    res = solver(robot).solve(**d)
     torch.cuda.synchronize()
-    model = load_model("unitree_go2")
-    idx = [1092, 23275, 26327, 2028, 22513]
+    assert (res.status.cpu().numpy() == 0).all()
+    model = load_model(robot)
+    idx = HARDEST[robot]
     ref = []
     for e in idx:
         args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         ref.append(torque(model, solve_exact(model, build_qp(model, *args), *args[:3]).x))
     nw, el = _rel_errors(res.tau.cpu().numpy()[idx], np.array(ref))
-    assert nw.max() <= NORM_TOL, (nw.max(), idx[int(np.argmax(nw))])
-    assert el.max() <= ELEM_TOL, (el.max(), idx[int(np.argmax(el))])
+    _check(nw, el, robot)
 
 
 @pytest.mark.parametrize("robot,nenv", [("unitree_go2", 65536), ("walter_sr", 8192)])

@@ -12,7 +12,7 @@ from osc_qp import build_qp, load_model, torque
 from qp_exact import solve_exact
 
 pytestmark = pytest.mark.gpu
-NORM_TOL = 1e-5
+NORM_TOL = 1e-9          # achieved bound of tests/test_gpu_parity.py (refined solves)
 
 
 def _oracle_tau(robot, d, e):
