@@ -920,9 +920,53 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // Slot-1 lanes past N (N < 32) hold a copy of column N-1 (the caller loads jj1 = N-1 there);
 // they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
 // finite, and never a broadcast source.
+#ifndef OSC_LDL_OVERLAP
+#define OSC_LDL_OVERLAP 1
+#endif
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
+#if OSC_LDL_OVERLAP
+  // Pivot k + 1 is final once step k has updated row k + 1 (its first FMA pair), so its
+  // broadcast, reciprocal and multipliers are issued right there and overlap the rest of step
+  // k's trailing update instead of waiting behind it (a lone wave otherwise stalls ~8 dependent
+  // f64 latencies per pivot).  Same operations, same order per value: bitwise-identical factor.
+  auto prep = [&](auto kc, double& t0, double& t1) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    const double own = (s == 0) ? c0[k] : c1[k];
+    const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
+    const double inv = recip1(dk);
+    sdinv[k] = inv;
+    t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(-c0[k] * inv);
+    constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
+    t1 = keep_lanes<rows_mask(kT1)>(-c1[k] * inv);
+  };
+  double t0n, t1n;
+  prep(std::integral_constant<int, 0>{}, t0n, t1n);
+  static_for<0, N>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    const double t0 = t0n, t1 = t1n;
+    auto upd = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      // the first update of a step reads a row the previous step may have written only a
+      // couple of instructions earlier (late pivots): guarded
+      constexpr bool kNop = (i == k + 1);
+      if constexpr (s == 0) {
+        fmac_bcast<kl, kNop>(c1[i], c0[i], t1);
+        if constexpr (k < kRow - 1) fmac_bcast_self<kl>(c0[i], t0);
+      } else {
+        fmac_bcast_self<kl, kNop>(c1[i], t1);
+      }
+    };
+    if constexpr (k + 1 < N) {
+      upd(std::integral_constant<int, k + 1>{});
+      prep(std::integral_constant<int, k + 1>{}, t0n, t1n);
+      static_for<k + 2, N>(upd);
+    }
+  });
+#else
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
@@ -948,6 +992,7 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
       }
     });
   });
+#endif
   wave_sync();
   dinv0 = sdinv[l];
   dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
@@ -1015,10 +1060,30 @@ struct RefineLds {
   static constexpr int GD = HD + D::NV * D::NV;
   static constexpr int SIZE = GD + even(D::NV);   // = W_SOL - W_X in the workspace
 };
-template <class D, bool SMALL, bool REFINE = false>
+// Refinement modes of the IPM body: none (the interior point alone; a torque-coordinate model
+// then hands its result to osc_refine_kernel through W_SOL), the refinement pass alone
+// (osc_refine_kernel), or both in one wavefront (one-wave variant: no hand-off, no second launch).
+constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
+#ifndef OSC_FUSE_REFINE
+#define OSC_FUSE_REFINE 1
+#endif
+template <class D, bool SMALL, int RF>
+constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
+  return SMALL && RF != kRfOnly && hr_fits_lds<D>();
+}
+// LDS doubles per env beyond the interior point's layout: the refinement's [X | H_dv | f_dv]
+// block, except that a fused pass with Hr in LDS moves X into Hr's region once the first K_A is
+// assembled (registers hold it from then on) and only keeps [H_dv | f_dv] apart.
+template <class D, bool SMALL, int RF>
+constexpr int refine_lds_extra() {
+  if constexpr (RF == kRfNone || !D::TY) return 0;
+  else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())
+    return RefineLds<D>::SIZE - RefineLds<D>::HD;
+  else return RefineLds<D>::SIZE;
+}
+template <class D, bool SMALL, int RF = kRfNone>
 constexpr int ipm_lds_doubles() {
-  constexpr int il = IpmLayout<D, SMALL && !REFINE && hr_fits_lds<D>()>::IL +
-                     (REFINE ? RefineLds<D>::SIZE : 0);
+  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>();
   return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
 }
 
@@ -1026,7 +1091,7 @@ constexpr int ipm_lds_doubles() {
 // doubles of LDS.  Wrapped by osc_ipm_kernel (one model) and osc_ipm_pair_kernel (two models).
 // WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
 // is unchanged by it: the two-wave Go2 variant would otherwise spill more).
-template <class D, bool SMALL, bool WARM, bool REFINE = false>
+template <class D, bool SMALL, bool WARM, int RF_ = kRfNone>
 __device__ __forceinline__ void ipm_block(
     const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
@@ -1034,9 +1099,11 @@ __device__ __forceinline__ void ipm_block(
     int fixup, double* __restrict__ sm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
                 MI = D::MI, NRL = D::NRL;
-  constexpr bool HRL = SMALL && !REFINE && hr_fits_lds<D>();
+  constexpr int RF = D::TY ? RF_ : kRfNone;   // refinement exists in torque coordinates only
+  constexpr bool REFINE = RF == kRfOnly;      // the refinement pass alone (no interior point)
+  if constexpr (RF_ == kRfOnly && !D::TY) return;
+  constexpr bool HRL = ipm_hrl<D, SMALL, RF>();
   using LY = IpmLayout<D, HRL>;
-  if constexpr (REFINE && !D::TY) return;   // refinement exists in torque coordinates only
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
   const int env_raw = blk * kEnvPerWave + grp;
@@ -1051,9 +1118,13 @@ __device__ __forceinline__ void ipm_block(
     write_out = valid && (!fixup || redo);
   }
 
-  constexpr int kEnvLds = LY::IL + (REFINE ? RefineLds<D>::SIZE : 0);
+  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>();
   double* B = sm + grp * kEnvLds;
-  double* sRef = B + LY::IL;   // REFINE: [X | H_dv | f_dv] of this env
+  // refinement: [X | H_dv | f_dv] of this env; a fused pass with Hr in LDS keeps X in Hr's region
+  constexpr bool kXinHr = RF == kRfFused && HRL;
+  double* sRX = kXinHr ? B + LY::I_HR : B + LY::IL + RefineLds<D>::X;
+  double* sRH = kXinHr ? B + LY::IL : B + LY::IL + RefineLds<D>::HD;
+  double* sRG = sRH + (RefineLds<D>::GD - RefineLds<D>::HD);
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -1387,7 +1458,7 @@ __device__ __forceinline__ void ipm_block(
     {
       Batch2<RefineLds<D>::SIZE / 2, kRow> bx;
       bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X, l);
-      bx.store(sRef, l);
+      bx.store(sRX, l);
     }
     const double* sol = ws + static_cast<size_t>(env) * D::WS + D::W_SOL;
     y0 = sol[j0];
@@ -1686,7 +1757,7 @@ __device__ __forceinline__ void ipm_block(
     STAMP_END(7);
   }
   STAMP_STORE();
-  if constexpr (D::TY && !REFINE) {   // hand the result to the refinement kernel
+  if constexpr (D::TY && RF == kRfNone) {   // hand the result to the refinement kernel
     if (write_out) {
       // (the W_SOL block is written here and read by nothing else in this kernel)
       double* sol = const_cast<double*>(ws) + static_cast<size_t>(env) * D::WS + D::W_SOL;
@@ -1714,7 +1785,7 @@ __device__ __forceinline__ void ipm_block(
   // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
   // discarded.
   bool refined = false;
-  if constexpr (D::TY && REFINE) {
+  if constexpr (D::TY && RF != kRfNone) {
     const bool mine = valid && st == OSC_SOLVE_OK;
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
@@ -1729,12 +1800,31 @@ __device__ __forceinline__ void ipm_block(
       const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg;
       double ya0 = y0, ya1 = y1;
       bool viol_env = false;
+      const double* wenv = ws + static_cast<size_t>(env) * D::WS;
+      if constexpr (RF == kRfFused) {
+        // this env's [X | H_dv | f_dv] (HRL: [H_dv | f_dv]; X follows once Hr's region is free)
+        constexpr int kFrom = kXinHr ? RefineLds<D>::HD : 0;
+        static_assert((RefineLds<D>::SIZE - kFrom) % 2 == 0 && (D::W_X + kFrom) % 2 == 0,
+                      "16-byte staging");
+        Batch2<(RefineLds<D>::SIZE - kFrom) / 2, kRow> bx;
+        bx.load(wenv + D::W_X + kFrom, l);
+        bx.store(kXinHr ? sRH : sRX, l);
+      }
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
       for (int round = 0; round < 3; ++round) {
-        if (round > 0) {
-          load_hr();   // c0 / c1 hold the last round's factor
+        if (round > 0) {   // c0 / c1 hold the last round's factor
+          if constexpr (kXinHr) {
+            // Hr's LDS region holds X now: Hr columns from the (L2-resident) workspace
+#pragma unroll
+            for (int i = 0; i < NY; ++i) {
+              c0[i] = wsw[lane_off + static_cast<unsigned>(i * NY + j0)];
+              c1[i] = wsw[lane_off + static_cast<unsigned>(i * NY + jj1)];
+            }
+          } else {
+            load_hr();
+          }
         }
 #pragma unroll
         for (int t = 0; t < NRL; ++t) sDr[l + kRow * t] = Dr[t];
@@ -1774,6 +1864,15 @@ __device__ __forceinline__ void ipm_block(
             c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
           }
         }
+        if constexpr (kXinHr) {
+          if (round == 0) {   // K_A is in registers: X takes Hr's region
+            static_assert(D::NV * D::NY1P <= even(NY * NY) && D::W_X % 2 == 0, "X in Hr's region");
+            Batch2<D::NV * D::NY1P / 2, kRow> bx;
+            bx.load(wenv + D::W_X, l);
+            wave_sync();   // every lane's Hr reads (load_hr) are done
+            bx.store(sRX, l);
+          }
+        }
         wave_sync();
         ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
         wave_sync();
@@ -1783,7 +1882,7 @@ __device__ __forceinline__ void ipm_block(
           for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
             const int rr = l + kRow * t;
             if (rr < NV) {
-              const double* xr = sRef + RefineLds<D>::X + rr * NY1P;
+              const double* xr = sRX + rr * NY1P;
               double a = xr[NY];
 #pragma unroll
               for (int i = 0; i < NY; ++i) a = fma(xr[i], sVy[i], a);
@@ -1798,8 +1897,8 @@ __device__ __forceinline__ void ipm_block(
             const int rr = l + kRow * t;
             gxr[t] = 0.0;
             if (rr < NV) {
-              const double* hr = sRef + RefineLds<D>::HD + rr * NV;
-              double a = sRef[RefineLds<D>::GD + rr];
+              const double* hr = sRH + rr * NV;
+              double a = sRG[rr];
 #pragma unroll
               for (int i = 0; i < NV; ++i) a = fma(hr[i], sXb[i], a);
               gxr[t] = a;
@@ -1816,8 +1915,8 @@ __device__ __forceinline__ void ipm_block(
           double r0 = (j0 < NU ? wu : wz) * ya0, r1 = (jj1 < NU ? wu : wz) * ya1;
 #pragma unroll
           for (int i = 0; i < NV; ++i) {
-            r0 = fma(sRef[RefineLds<D>::X + i * NY1P + j0], sDr[i], r0);
-            r1 = fma(sRef[RefineLds<D>::X + i * NY1P + jj1], sDr[i], r1);
+            r0 = fma(sRX[i * NY1P + j0], sDr[i], r0);
+            r1 = fma(sRX[i * NY1P + jj1], sDr[i], r1);
           }
           double gm0, gm1;
           GTw2(sVr, gm0, gm1);
@@ -1876,7 +1975,7 @@ __device__ __forceinline__ void ipm_block(
   }
 
   // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
-  if (REFINE && !refined) write_out = false;   // the interior point's outputs stand
+  if (REFINE && !refined) write_out = false;   // the interior point kernel's outputs stand
   if (l < NU) {
     double tq = D::TY ? sVy[l] : sU[l * NY1P + NY];
 #pragma unroll
@@ -1931,14 +2030,16 @@ __device__ __forceinline__ void ipm_block(
   }
 }
 
-template <class D, bool SMALL, bool WARM, bool REFINE = false>
+template <class D, bool SMALL, bool WARM, int RF = kRfNone>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
     int fixup) {
-  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL>()];
-  ipm_block<D, SMALL, WARM, REFINE>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
+  // one-wave variant: four workgroups per CU (160 KB of LDS), never five
+  static_assert(!SMALL || ipm_lds_doubles<D, SMALL, RF>() * 8 <= 160 * 1024 / 4, "IPM LDS");
+  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, RF>()];
+  ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                     gstatus, giters, gwarm, fixup, sm);
 }
 
@@ -1949,8 +2050,8 @@ template <class D, bool SMALL>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_refine_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx) {
-  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, true>()];
-  ipm_block<D, SMALL, false, true>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
+  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, kRfOnly>()];
+  ipm_block<D, SMALL, false, kRfOnly>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                    nullptr, nullptr, nullptr, 0, sm);
 }
 
@@ -1959,17 +2060,17 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_refine_kernel(
 // in order, so with the slower model first the faster model's wavefronts fill the SIMDs that
 // the first model's early finishers free (its iteration-count tail) -- two grids on two streams
 // instead split the SIMDs between the models and each pays its own tail.
-template <class DA, class DB, bool REFINE = false>
+template <class DA, class DB, int RF = kRfNone>
 __global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, PairArgs B) {
   __shared__ __attribute__((aligned(16))) double
-      sm[cmax(ipm_lds_doubles<DA, true, REFINE>(), ipm_lds_doubles<DB, true, REFINE>())];
+      sm[cmax(ipm_lds_doubles<DA, true, RF>(), ipm_lds_doubles<DB, true, RF>())];
   const int nbA = (A.nenv + kEnvPerWave - 1) / kEnvPerWave;
   const int blk = static_cast<int>(blockIdx.x);
   if (blk < nbA)
-    ipm_block<DA, true, false, REFINE>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status,
+    ipm_block<DA, true, false, RF>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status,
                                        A.iters, nullptr, 0, sm);
   else
-    ipm_block<DB, true, false, REFINE>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x,
+    ipm_block<DB, true, false, RF>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x,
                                        B.status, B.iters, nullptr, 0, sm);
 }
 
@@ -2153,8 +2254,13 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     if (warm != nullptr && status == nullptr)
       status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
     const bool small = nenv <= model->small_batch_max;
+    // The one-wave cold solve runs the refinement in the same wavefront (kRfFused).
+    const bool fused = OSC_FUSE_REFINE && small && warm == nullptr && D::TY && model->refine;
     if (warm == nullptr) {
-      if (small)
+      if (fused)
+        hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+      else if (small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
       else
@@ -2170,7 +2276,7 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
                              model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
       }
     }
-    if (D::TY && model->refine) {
+    if (D::TY && model->refine && !fused) {
       if (small)
         hipLaunchKernelGGL((osc_refine_kernel<D, true>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x);
@@ -2265,9 +2371,11 @@ void launch_pair(const osc_batch_job& a, const osc_batch_job& b, hipStream_t s) 
                      dim3(kWave), 0, s, A, B);
   const unsigned nb = static_cast<unsigned>((a.nenv + kEnvPerWave - 1) / kEnvPerWave +
                                             (b.nenv + kEnvPerWave - 1) / kEnvPerWave);
-  hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB>), dim3(nb), dim3(kWave), 0, s, A, B);
+  // one-wave interior point of both models with the refinement in the same wavefront
   if (a.model->refine || b.model->refine)
-    hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB, true>), dim3(nb), dim3(kWave), 0, s, A, B);
+    hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB, kRfFused>), dim3(nb), dim3(kWave), 0, s, A, B);
+  else
+    hipLaunchKernelGGL((osc_ipm_pair_kernel<DA, DB>), dim3(nb), dim3(kWave), 0, s, A, B);
 }
 
 }  // namespace

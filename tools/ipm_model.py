@@ -153,6 +153,34 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         s += ds_; lam += dl_
         sl = s @ lam
         s += 0.5 * sl / lam.sum(); lam += 0.5 * sl / s.sum()
+    elif any(v.startswith("lsR") for v in variant):
+        # scaled least-squares start: rows weighted by R_r = c x (Hr diagonal under row r), so
+        # the start sees the bounds at the objective's own scale; lambda0 = R (G y0 - h) is the
+        # penalty estimate of the multipliers.  Shifts as the kernel's, lambda's in R units.
+        v = [v for v in variant if v.startswith("lsR")][0]
+        c = float(v[3:])
+        keep = ~np.isclose(h, BIG_NUMBER)
+        dgh = np.abs(np.diag(Hr))
+        R = c * (np.abs(G) @ dgh) / np.maximum(np.abs(G).sum(axis=1), 1e-300)
+        Gs, hs, Rs = G[keep], h[keep], R[keep]
+        y = np.linalg.solve(Hr + Gs.T @ (Rs[:, None] * Gs), -g + Gs.T @ (Rs * hs))
+        zr = G @ y - h
+        ap = max(zr.max(), 0.0)
+        s = -zr + (1.0 + ap if zr.max() >= 0 else 0.0)
+        zl = zr * (R if "lsRlam" not in variant else 1.0)
+        rowc = [float(v[4:]) for v in variant if v.startswith("rowc") and len(v) > 4]
+        if rowc:                                   # per-row floors, products >= c0 x mean
+            s = np.maximum(-zr, 1.0)
+            mu0 = rowc[0] * np.abs(zl).mean()
+            lam = np.maximum(zl, mu0 / s)
+            s = np.maximum(s, mu0 / lam)
+        elif "lsRdual1" in variant:                  # lambda shift in units of R
+            ad = max((-zr).max(), 0.0)
+            lam = R * (zr + 1.0 + ad)
+        else:
+            ad = (-zl).max()
+            lam = zl + (1.0 + ad if ad >= 0 else 0.0)
+        eta = 0.99
     elif "init_row1" in variant:               # per-row: slack and multiplier each >= 1
         s, lam = np.maximum(-zr, 1.0), np.maximum(zr, 1.0)
     elif "init_rowc" in variant:               # per-row slack; lambda centred on mu0

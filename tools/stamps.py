@@ -6,8 +6,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["OSC_LIB_PATH"] = os.path.join(REPO, "operational-space-control_amd", "lib",
-                                          "libosc_batch_stamps.so")
+os.environ["OSC_LIB_PATH"] = os.environ.get("OSC_STAMPS_LIB") or os.path.join(
+    REPO, "operational-space-control_amd", "lib", "libosc_batch_stamps.so")
 sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
