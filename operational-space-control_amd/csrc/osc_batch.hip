@@ -921,7 +921,7 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
 // finite, and never a broadcast source.
 #ifndef OSC_LDL_OVERLAP
-#define OSC_LDL_OVERLAP 1
+#define OSC_LDL_OVERLAP 0   // measured ~1 % slower at Go2 4,096 (tools/ab_run.sh)
 #endif
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
