@@ -71,6 +71,7 @@ struct DevParams {
   int32_t max_iter;
   int32_t refine_steps;              // full-space refinement steps after the interior point
   double refine_penalty;             // active-row penalty, x max diag(Hr)
+  double w_sqrt[6 * OSC_MAX_SITES];  // sqrt(w_row): setup_rows stages W^1/2 [J | e]
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -920,6 +921,566 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // Slot-1 lanes past N (N < 32) hold a copy of column N-1 (the caller loads jj1 = N-1 there);
 // they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
 // finite, and never a broadcast source.
+// ==================== kernel 1b: reduced QP, four environments per wavefront ================
+// Torque coordinates only.  The interior point's mapping: one 16-lane DPP row per environment,
+// so every serial step (base-block LDL^T, the Schur complement's factorisation and solves) is
+// done once per env instead of once per lane or per row of a 64-lane wave, and the whole batch
+// is resident at once at one wave per SIMD (4,096 envs on 1,024 SIMDs: one round, where the
+// 64-lane kernel needs two at two waves per SIMD).  Same closed forms as setup_env; the sums run
+// in another order (J's rows are staged contact rows last), so results agree to rounding.
+// LDS per env (doubles); regions are reused phase by phase:
+//   stage   A = [J | e | 0] (S x NAP, rows in slot order) | M | C
+//   Ha      H_dv | f_dv over A's rows (A is dead once every lane holds its Ha tiles)
+//   X       X_b / U, then X (NV x NY1P) after H_dv | f_dv
+//   T1      H_dv X (+ f_dv in the affine column) after X
+//   out     g | Hr (the interior point's LDS layout) over H_dv | f_dv | X
+// An opaque 0 that depends on v: LDS addresses offset by it cannot be issued before v exists
+// (bounds the loads in flight where the compiler would otherwise hoist a whole unrolled loop's).
+__device__ __forceinline__ unsigned after(double v) {
+  unsigned z = 0;
+  asm volatile("" : "+v"(z) : "v"(v));
+  return z;
+}
+
+template <class D>
+struct Setup4Lds {
+  static constexpr int NV = D::NV, NY1P = D::NY1P;
+  static constexpr int A = 0;
+  static constexpr int M = A + D::S * D::NAP;
+  static constexpr int C = M + NV * NV;
+  static constexpr int JC = C + even(NV);            // unscaled Jc rows (3 NC x NV) + a dump pair
+  static constexpr int STAGE_END = JC + 3 * D::NC * NV + 2;
+  static constexpr int H = 0;
+  static constexpr int F = H + NV * NV;
+  static constexpr int X = F + even(NV);
+  static constexpr int T1 = X + NV * NY1P;
+  static constexpr int END = T1 + NV * NY1P;
+  static constexpr int SIZE = even(cmax(STAGE_END, END));
+  static constexpr int OUT = even(D::NY) + even(D::NY * D::NY);   // g | Hr
+  static_assert(OUT <= X + NV * NY1P || OUT <= SIZE, "g | Hr fits the region");
+};
+template <class D>
+constexpr bool setup4_fits() {   // four envs per wave in one SIMD's share of a CU's LDS (40 KB)
+  return D::TY && D::NU <= kRow && D::NY1 <= 2 * kRow && D::NV <= 2 * kRow &&
+         Setup4Lds<D>::SIZE * kEnvPerWave * 8 <= 160 * 1024 / 4;
+}
+// Task row staged in LDS slot s: the rows that are not contact translational rows first, then
+// the 3 NC contact rows in order -- Jc's rows end up in one contiguous block.
+template <class D>
+constexpr int setup4_row_of_slot(int s) {
+  constexpr int JC0 = 3 * (D::NS - D::NC), NZ = 3 * D::NC;
+  return s < D::S - NZ ? (s < JC0 ? s : s + NZ) : JC0 + (s - (D::S - NZ));
+}
+template <class D>
+constexpr int setup4_slot_of_row(int r) {
+  constexpr int JC0 = 3 * (D::NS - D::NC), NZ = 3 * D::NC;
+  return r < JC0 ? r : (r < JC0 + NZ ? D::S - NZ + (r - JC0) : r - NZ);
+}
+
+// One wavefront's four environments (envs 4 blk + grp).  `sm` holds kEnvPerWave regions of
+// `stride` doubles; on return each env's region starts with its g | Hr (interior-point layout)
+// and the workspace holds X | H_dv | f_dv (refinement, outputs).  Rows of envs past nenv replay
+// env nenv - 1 and write nothing.
+template <class D>
+__device__ __forceinline__ void setup_rows(
+    const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gM,
+    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
+    double* __restrict__ sm, int stride) {
+  using L4 = Setup4Lds<D>;
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
+                NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NAP = D::NAP, NZ = 3 * NC;
+  static_assert(D::TY && NV % 2 == 0 && NY1P % 2 == 0 && NAP == NV + 2, "setup_rows layout");
+  const int lane = threadIdx.x;
+  const int grp = lane / kRow, l = lane % kRow;
+  const int env_raw = blk * kEnvPerWave + grp;
+  const bool valid = env_raw < nenv;
+  const int env = valid ? env_raw : nenv - 1;
+  double* E = sm + grp * stride;
+  double* sA = E + L4::A;
+  double* sM = E + L4::M;
+  double* sC = E + L4::C;
+  double* wsenv = ws + static_cast<size_t>(env) * D::WS;
+  STAMP_DECL
+  STAMP_BEGIN();
+
+  // ---------------- stage: every load in flight first ----------------
+  // A = W^1/2 [J | e | 0]: Ha = 2 A'A needs no weight inside its row loop
+  Batch2<S * NV / 2, kRow> bJ;
+  double wsq[Batch2<S * NV / 2, kRow>::T];
+#pragma unroll
+  for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
+    const int c = l + t * kRow;
+    wsq[t] = P->w_sqrt[(c < S * NV / 2 ? c : S * NV / 2 - 1) / (NV / 2)];
+  }
+  Batch2<NV * NV / 2, kRow> bM;
+  Batch2<NV / 2, kRow> bC;
+  bJ.load(gJ + static_cast<size_t>(env) * S * NV, l);
+  bM.load(gM + static_cast<size_t>(env) * NV * NV, l);
+  bC.load(gC + static_cast<size_t>(env) * NV, l);
+  double mk[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) mk[k] = gmask[static_cast<size_t>(env) * NC + k];
+  constexpr int TE = (S + kRow - 1) / kRow;
+  double eb[TE], et[TE], ew[TE];
+#pragma unroll
+  for (int q = 0; q < TE; ++q) {
+    const int r = (l + q * kRow < S) ? l + q * kRow : S - 1;
+    const int half = r / (3 * NS), rr = r % (3 * NS);
+    ew[q] = P->w_sqrt[r];
+    eb[q] = gb[static_cast<size_t>(env) * S + r];
+    et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+  }
+  // contact rows also unscaled (X_b, U need Jc itself); other chunks to the dump pair
+  {
+    constexpr int JC0 = 3 * (NS - NC);
+    double2* jc2 = reinterpret_cast<double2*>(E + L4::JC);
+#pragma unroll
+    for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
+      const int c = l + t * kRow;
+      const int cc = c < S * NV / 2 ? c : S * NV / 2 - 1;
+      const int rc = cc / (NV / 2) - JC0;
+      const bool in = rc >= 0 && rc < NZ;
+      jc2[in ? rc * (NV / 2) + cc % (NV / 2) : NZ * NV / 2] = bJ.v[t];
+    }
+  }
+  // J row r -> A row setup4_slot_of_row(r), 16-byte chunks (NV / 2 per row), scaled by sqrt(w_r)
+#pragma unroll
+  for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
+    bJ.v[t].x *= wsq[t];
+    bJ.v[t].y *= wsq[t];
+  }
+  bJ.store(sA, l, [](int c) {
+    const int r = c / (NV / 2);
+    return setup4_slot_of_row<D>(r) * (NAP / 2) + c % (NV / 2);
+  });
+  bM.store(sM, l);
+  bC.store(sC, l);
+#pragma unroll
+  for (int q = 0; q < TE; ++q) {   // e = b - t and the zero pad column (lanes past S rewrite row S-1)
+    const int r = (l + q * kRow < S) ? l + q * kRow : S - 1;
+    const int sl = setup4_slot_of_row<D>(r);
+    *reinterpret_cast<double2*>(sA + sl * NAP + NV) = make_double2((eb[q] - et[q]) * ew[q], 0.0);
+  }
+  wave_sync();
+
+  STAMP_END(0);
+  STAMP_BEGIN();
+  // ---------------- Ha = 2 [J e]' W [J e] (upper 2x2 tiles; the e.e corner is not needed) --------
+  constexpr int NA2 = NAP / 2;
+  constexpr int NTA = NA2 * (NA2 + 1) / 2 - 1;
+  constexpr int TA = (NTA + kRow - 1) / kRow;
+  // rows outer, the lane's TA tiles inner: TA x 2 loads and TA x 4 accumulators live at a time
+  int hi0[TA], hj0[TA];
+#pragma unroll
+  for (int t = 0; t < TA; ++t) {
+    upper_pair<NA2>((l + t * kRow < NTA) ? l + t * kRow : NTA - 1, hi0[t], hj0[t]);
+    hi0[t] *= 2;
+    hj0[t] *= 2;
+  }
+  double ha[TA][4];
+#pragma unroll
+  for (int t = 0; t < TA; ++t) ha[t][0] = ha[t][1] = ha[t][2] = ha[t][3] = 0.0;
+  // software-pipelined: row s + 1's reads are issued before row s's FMAs
+  double2 hx[TA], hy[TA];
+#pragma unroll
+  for (int t = 0; t < TA; ++t) {
+    hx[t] = *reinterpret_cast<const double2*>(sA + hi0[t]);
+    hy[t] = *reinterpret_cast<const double2*>(sA + hj0[t]);
+  }
+#pragma unroll 2
+  for (int s = 0; s < S; ++s) {
+    const double* an = sA + (s + 1 < S ? s + 1 : s) * NAP;
+    double2 nx[TA], ny[TA];
+#pragma unroll
+    for (int t = 0; t < TA; ++t) {
+      nx[t] = *reinterpret_cast<const double2*>(an + hi0[t]);
+      ny[t] = *reinterpret_cast<const double2*>(an + hj0[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < TA; ++t) {
+      ha[t][0] = fma(hx[t].x, hy[t].x, ha[t][0]);
+      ha[t][1] = fma(hx[t].x, hy[t].y, ha[t][1]);
+      ha[t][2] = fma(hx[t].y, hy[t].x, ha[t][2]);
+      ha[t][3] = fma(hx[t].y, hy[t].y, ha[t][3]);
+      hx[t] = nx[t];
+      hy[t] = ny[t];
+    }
+  }
+  wave_sync();   // A is dead: H_dv | f_dv take its place
+  double* sH = E + L4::H;
+  double* sF = E + L4::F;
+  {
+    // branch-free scatter: every entry goes somewhere; the ones not wanted (pad column, the
+    // mirrored half of a diagonal tile) to a slot X overwrites later
+    const double wr2 = 2.0 * P->w_reg;
+    double* dump = E + L4::X + l;   // one slot per lane: a shared one serialises the stores
+    auto put = [&](int i, int j, bool keep, double v) {
+      const bool hj = keep && j < NV, fj = keep && j == NV;
+      v = 2.0 * v + ((i == j) ? wr2 : 0.0);
+      double* p1 = hj ? sH + i * NV + j : (fj ? sF + i : dump);
+      double* p2 = hj ? sH + j * NV + i : dump;
+      *p1 = v;
+      *p2 = v;
+    };
+#pragma unroll
+    for (int t = 0; t < TA; ++t) {
+      const bool ok = l + t * kRow < NTA;
+      const int i0 = hi0[t], j0 = hj0[t];
+      put(i0, j0, ok, ha[t][0]);
+      put(i0, j0 + 1, ok, ha[t][1]);
+      put(i0 + 1, j0, ok && i0 != j0, ha[t][2]);
+      put(i0 + 1, j0 + 1, ok, ha[t][3]);
+    }
+  }
+  wave_sync();
+
+  STAMP_END(1);
+  STAMP_BEGIN();
+  // ---------------- X_b = M_bb^-1 [-M_ba | Jc_b | -C_b], U = M_ab X_b + [M_aa | -Jc_a | C_a] ----
+  // Lane l: columns c = l and l + 16 of [y; 1] (padding column and past it: zeros).  The base
+  // block's LDL^T is formed per lane (NB^3 / 6 flops) from broadcast LDS reads of M.
+  double xbs[2][NB], us[2][NU];
+  {
+    double Lb[NB][NB];
+    double dinv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j <= i; ++j) Lb[i][j] = sM[i * NV + j];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      dinv[k] = recip1(Lb[k][k]);
+#pragma unroll
+      for (int i = k + 1; i < NB; ++i) {
+        const double lik = Lb[i][k] * dinv[k];
+#pragma unroll
+        for (int j = k + 1; j <= i; ++j) Lb[i][j] = fma(-lik, Lb[j][k], Lb[i][j]);
+      }
+#pragma unroll
+      for (int i = k + 1; i < NB; ++i) Lb[i][k] *= dinv[k];
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int c = l + kRow * sl;
+      const bool cu = c < NU, cz = !cu && c < NY, live = c < NY1;
+      const int kz = cz ? (c - NU) / 3 : 0;
+      double mkz = mk[0];
+#pragma unroll
+      for (int k = 1; k < NC; ++k) mkz = (kz == k) ? mk[k] : mkz;
+      const bool pinned = cz && mkz == 0.0;
+      const int cc = live ? c : NY;   // a readable column for lanes that write zeros
+      const bool ccu = cc < NU, ccz = !ccu && cc < NY;
+      const double* sJc = E + L4::JC;
+      const double* xp = ccu ? sM + NB + cc : (ccz ? sJc + (cc - NU) * NV : sC);
+      const int xs = ccu ? NV : 1;
+      const double xsg = ccz ? 1.0 : -1.0;
+      const double* up = ccu ? sM + NB * NV + NB + cc : (ccz ? sJc + (cc - NU) * NV + NB : sC + NB);
+      const double usg = ccz ? -1.0 : 1.0;
+      double x[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) x[i] = (pinned || !live) ? 0.0 : xsg * xp[i * xs];
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int i = k + 1; i < NB; ++i) x[i] = fma(-Lb[i][k], x[k], x[i]);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) x[k] *= dinv[k];
+#pragma unroll
+      for (int k = NB - 1; k >= 0; --k)
+#pragma unroll
+        for (int i = 0; i < k; ++i) x[i] = fma(-Lb[k][i], x[k], x[i]);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) xbs[sl][i] = x[i];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) {
+        double acc = (pinned || !live) ? 0.0 : usg * up[a * xs];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
+        us[sl][a] = acc;
+      }
+    }
+  }
+  wave_sync();   // M, C and Jc are dead: X_b | U into X's rows
+  double* sX = E + L4::X;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int c = l + kRow * sl;
+    if (c < NY1P) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = xbs[sl][i];
+#pragma unroll
+      for (int a = 0; a < NU; ++a) sX[(NB + a) * NY1P + c] = us[sl][a];
+    }
+  }
+  wave_sync();
+
+  STAMP_END(2);
+  STAMP_BEGIN();
+  // ---------------- Schur complement S = U[:, :NU] = L D L' in the env's row; X = [x_b; x_a] -----
+  {
+    double col[NU];
+    const int lj = l < NU ? l : 0;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) col[i] = sX[(NB + i) * NY1P + lj];
+    double dj = 1.0;
+    static_for<0, NU>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      const double rk = recip1(bcast_guarded<k>(col[k]));
+      if (l == k) dj = rk;
+      const double m = (l > k) ? -col[k] * rk : 0.0;
+      static_for<k + 1, NU>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        fmac_bcast_self<k, true>(col[i], m);
+      });
+    });
+    double dinv[NU];
+    static_for<0, NU>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      dinv[k] = bcast_guarded<k>(dj);
+    });
+    double xa0[NU], xa1[NU], xb0[NB], xb1[NB], xbc[NB];
+    {
+      const int c0 = l, c1 = l + kRow;
+      const int r0 = c0 < NY1 ? c0 : NY, r1 = c1 < NY1 ? c1 : NY;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const double u0 = sX[(NB + i) * NY1P + r0], u1 = sX[(NB + i) * NY1P + r1];
+        xa0[i] = (c0 < NU) ? ((i == c0) ? 1.0 : 0.0) : -u0;
+        xa1[i] = (c1 < NU) ? ((i == c1) ? 1.0 : 0.0) : -u1;
+      }
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        xb0[r] = (c0 < NU) ? 0.0 : sX[r * NY1P + r0];
+        xb1[r] = (c1 < NU) ? 0.0 : sX[r * NY1P + r1];
+        xbc[r] = sX[r * NY1P + lj];   // X_b[:, j]: the DPP source of lane j
+      }
+    }
+    static_for<0, NU>([&](auto K) {   // L z = r
+      constexpr int k = decltype(K)::value;
+      const double t0 = -xa0[k] * dinv[k], t1 = -xa1[k] * dinv[k];
+      static_for<k + 1, NU>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        fmac_bcast2<k, false>(xa0[i], xa1[i], col[i], t0, t1);
+      });
+    });
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      xa0[k] *= dinv[k];
+      xa1[k] *= dinv[k];
+    }
+    static_for<0, NU - 1>([&](auto J) {   // L' x = y
+      constexpr int i = NU - 2 - decltype(J)::value;
+      double a0 = 0.0, a1 = 0.0;
+      static_for<i + 1, NU>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        fmac_bcast2<i, false>(a0, a1, col[k], xa0[k], xa1[k]);
+      });
+      xa0[i] = fma(-dinv[i], a0, xa0[i]);
+      xa1[i] = fma(-dinv[i], a1, xa1[i]);
+    });
+    static_for<0, NU>([&](auto Q) {   // x_b += X_b[:, :NU] x_a
+      constexpr int q = decltype(Q)::value;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) fmac_bcast2<q, false>(xb0[r], xb1[r], xbc[r], xa0[q], xa1[q]);
+    });
+    wave_sync();   // every lane has read X_b and U
+    const int c0 = l, c1 = l + kRow;
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      sX[r * NY1P + c0] = c0 < NY1 ? xb0[r] : 0.0;
+      if (c1 < NY1P) sX[r * NY1P + c1] = c1 < NY1 ? xb1[r] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      sX[(NB + i) * NY1P + c0] = c0 < NY1 ? xa0[i] : 0.0;
+      if (c1 < NY1P) sX[(NB + i) * NY1P + c1] = c1 < NY1 ? xa1[i] : 0.0;
+    }
+  }
+  wave_sync();
+  STAMP_END(3);
+  STAMP_BEGIN();
+  // X and H_dv | f_dv -> workspace (refinement, outputs), coalesced
+  if (valid) {
+    static_assert(D::W_GD == D::W_HD + NV * NV && L4::F == L4::H + NV * NV, "H_dv | f_dv blocks");
+    constexpr int NX2 = NV * NY1P / 2, NH2 = (NV * NV + NV) / 2;
+    const double2* sx2 = reinterpret_cast<const double2*>(sX);
+    const double2* sh2 = reinterpret_cast<const double2*>(sH);
+    double2* wx2 = reinterpret_cast<double2*>(wsenv + D::W_X);
+    double2* wh2 = reinterpret_cast<double2*>(wsenv + D::W_HD);
+    for (int i = l; i < NX2; i += kRow) wx2[i] = sx2[i];
+    for (int i = l; i < NH2; i += kRow) wh2[i] = sh2[i];
+  }
+
+  STAMP_END(4);
+  STAMP_BEGIN();
+  // ---------------- T1 = H_dv X (+ f_dv in the affine column): 2x2 tiles --------------------
+  double* sT1 = E + L4::T1;
+  {
+    constexpr int NY2 = NY1P / 2, NR2 = NV / 2;
+    constexpr int NT = NR2 * NY2;
+    constexpr int TT = (NT + kRow - 1) / kRow;
+    int tr0[TT], tc0[TT];
+    double tt[TT][4];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      const int p = (l + t * kRow < NT) ? l + t * kRow : NT - 1;
+      tr0[t] = 2 * (p / NY2);
+      tc0[t] = 2 * (p % NY2);
+      const bool aff = tc0[t] == NY;   // affine column: T1 starts at f_dv
+      tt[t][0] = aff ? sF[tr0[t]] : 0.0;
+      tt[t][1] = 0.0;
+      tt[t][2] = aff ? sF[tr0[t] + 1] : 0.0;
+      tt[t][3] = 0.0;
+    }
+    // software-pipelined over i (H entries as column pairs: one 16-byte read per two i)
+    double2 ch0[TT], ch1[TT], cx0[TT], cx1[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      ch0[t] = *reinterpret_cast<const double2*>(sH + tr0[t] * NV);
+      ch1[t] = *reinterpret_cast<const double2*>(sH + (tr0[t] + 1) * NV);
+      cx0[t] = *reinterpret_cast<const double2*>(sX + tc0[t]);
+      cx1[t] = *reinterpret_cast<const double2*>(sX + NY1P + tc0[t]);
+    }
+#pragma unroll 1
+    for (int i = 0; i < NV; i += 2) {
+      const int in = i + 2 < NV ? i + 2 : i;
+      double2 nh0[TT], nh1[TT], nx0[TT], nx1[TT];
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        nh0[t] = *reinterpret_cast<const double2*>(sH + tr0[t] * NV + in);
+        nh1[t] = *reinterpret_cast<const double2*>(sH + (tr0[t] + 1) * NV + in);
+        nx0[t] = *reinterpret_cast<const double2*>(sX + in * NY1P + tc0[t]);
+        nx1[t] = *reinterpret_cast<const double2*>(sX + (in + 1) * NY1P + tc0[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        tt[t][0] = fma(ch0[t].x, cx0[t].x, tt[t][0]);
+        tt[t][1] = fma(ch0[t].x, cx0[t].y, tt[t][1]);
+        tt[t][2] = fma(ch1[t].x, cx0[t].x, tt[t][2]);
+        tt[t][3] = fma(ch1[t].x, cx0[t].y, tt[t][3]);
+        tt[t][0] = fma(ch0[t].y, cx1[t].x, tt[t][0]);
+        tt[t][1] = fma(ch0[t].y, cx1[t].y, tt[t][1]);
+        tt[t][2] = fma(ch1[t].y, cx1[t].x, tt[t][2]);
+        tt[t][3] = fma(ch1[t].y, cx1[t].y, tt[t][3]);
+        ch0[t] = nh0[t];
+        ch1[t] = nh1[t];
+        cx0[t] = nx0[t];
+        cx1[t] = nx1[t];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      if (l + t * kRow >= NT) continue;
+      *reinterpret_cast<double2*>(sT1 + tr0[t] * NY1P + tc0[t]) = make_double2(tt[t][0], tt[t][1]);
+      *reinterpret_cast<double2*>(sT1 + (tr0[t] + 1) * NY1P + tc0[t]) =
+          make_double2(tt[t][2], tt[t][3]);
+    }
+  }
+  wave_sync();
+
+  STAMP_END(5);
+  STAMP_BEGIN();
+  // ---------------- Hr | g = X' T1 + 2 (w_tau + w_reg) I_u + 2 w_reg I_z (upper 2x2 tiles) ------
+  constexpr int NY2 = NY1P / 2;
+  constexpr int NTH = NY2 * (NY2 + 1) / 2;
+  constexpr int TH = (NTH + kRow - 1) / kRow;
+  int ha0[TH], hb0[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    upper_pair<NY2>((l + t * kRow < NTH) ? l + t * kRow : NTH - 1, ha0[t], hb0[t]);
+    ha0[t] *= 2;
+    hb0[t] *= 2;
+  }
+  double hr[TH][4];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) hr[t][0] = hr[t][1] = hr[t][2] = hr[t][3] = 0.0;
+  double2 qx[TH], qt[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    qx[t] = *reinterpret_cast<const double2*>(sX + ha0[t]);
+    qt[t] = *reinterpret_cast<const double2*>(sT1 + hb0[t]);
+  }
+#pragma unroll 2
+  for (int r = 0; r < NV; ++r) {
+    const int rn = r + 1 < NV ? r + 1 : r;
+    double2 nx[TH], nt[TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      nx[t] = *reinterpret_cast<const double2*>(sX + rn * NY1P + ha0[t]);
+      nt[t] = *reinterpret_cast<const double2*>(sT1 + rn * NY1P + hb0[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      hr[t][0] = fma(qx[t].x, qt[t].x, hr[t][0]);
+      hr[t][1] = fma(qx[t].x, qt[t].y, hr[t][1]);
+      hr[t][2] = fma(qx[t].y, qt[t].x, hr[t][2]);
+      hr[t][3] = fma(qx[t].y, qt[t].y, hr[t][3]);
+      qx[t] = nx[t];
+      qt[t] = nt[t];
+    }
+  }
+  STAMP_END(6);
+  STAMP_BEGIN();
+  wave_sync();   // X and T1 are dead: g | Hr in the interior point's layout
+  {
+    double* sG = E;
+    double* sHr = E + even(NY);
+    double* dump = E + L4::T1 + l;   // T1 is dead here; one slot per lane
+    const double wu2 = 2.0 * (P->w_torque + P->w_reg);
+    const double wr2 = 2.0 * P->w_reg;
+    // z diagonal of a pinned contact: identity row (its X column is zero)
+    auto put = [&](int a, int b, bool keep, double acc) {
+      const bool hb = keep && b < NY, gb_ = keep && b == NY && a < NY;
+      const int kz = (a - NU) / 3;
+      double m = mk[0];
+#pragma unroll
+      for (int k = 1; k < NC; ++k) m = (kz == k) ? mk[k] : m;
+      const bool dg = a == b;
+      acc += dg ? ((a < NU) ? wu2 : wr2) : 0.0;
+      acc = (dg && a >= NU && m == 0.0) ? 1.0 : acc;
+      double* p1 = hb ? sHr + a * NY + b : (gb_ ? sG + a : dump);
+      double* p2 = hb ? sHr + b * NY + a : dump;
+      *p1 = acc;
+      *p2 = acc;
+    };
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      const bool ok = l + t * kRow < NTH;
+      const int a0 = ha0[t], b0 = hb0[t];
+      put(a0, b0, ok, hr[t][0]);
+      put(a0, b0 + 1, ok, hr[t][1]);
+      put(a0 + 1, b0, ok && a0 != b0, hr[t][2]);
+      put(a0 + 1, b0 + 1, ok, hr[t][3]);
+    }
+  }
+  wave_sync();
+  STAMP_END(7);
+  STAMP_STORE_SETUP();
+}
+
+// Standalone form: g | Hr copied from LDS to the workspace (the interior-point kernels read the
+// same layout as osc_setup_kernel writes).
+template <class D>
+__global__ __launch_bounds__(kWave, 1) void osc_setup4_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
+    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
+  static_assert(setup4_fits<D>(), "setup_rows LDS budget");
+  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * Setup4Lds<D>::SIZE];
+  const int blk = static_cast<int>(blockIdx.x);
+  setup_rows<D>(P, blk, nenv, gM, gC, gJ, gb, gT, gmask, ws, sm, Setup4Lds<D>::SIZE);
+  const int grp = threadIdx.x / kRow, l = threadIdx.x % kRow;
+  const int env = blk * kEnvPerWave + grp;
+  if (env < nenv) {
+    constexpr int N2 = (even(D::NY) + even(D::NY * D::NY)) / 2;
+    static_assert(D::W_G == 0 && D::W_HR == even(D::NY), "g | Hr workspace prefix");
+    const double2* s2 = reinterpret_cast<const double2*>(sm + grp * Setup4Lds<D>::SIZE);
+    double2* w2 = reinterpret_cast<double2*>(ws + static_cast<size_t>(env) * D::WS);
+    for (int i = l; i < N2; i += kRow) w2[i] = s2[i];
+  }
+}
+
 #ifndef OSC_LDL_OVERLAP
 #define OSC_LDL_OVERLAP 0   // measured ~1 % slower at Go2 4,096 (tools/ab_run.sh)
 #endif
@@ -1064,6 +1625,11 @@ struct RefineLds {
 // then hands its result to osc_refine_kernel through W_SOL), the refinement pass alone
 // (osc_refine_kernel), or both in one wavefront (one-wave variant: no hand-off, no second launch).
 constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
+// setup_rows (four envs per wavefront, one round at 4,096 envs) measured no faster than the
+// 64-lane osc_setup_kernel (Go2 4,096: 35.3 vs 33.7 us): off by default
+#ifndef OSC_SETUP4
+#define OSC_SETUP4 0
+#endif
 #ifndef OSC_FUSE_REFINE
 #define OSC_FUSE_REFINE 1
 #endif
@@ -2144,6 +2710,7 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
       hp.w_row[3 * d.ns + 3 * i + t] = d.w_rot[i];
     }
   }
+  for (int r = 0; r < 6 * d.ns; ++r) hp.w_sqrt[r] = std::sqrt(hp.w_row[r]);
   for (int i = 0; i < d.nu; ++i) {
     hp.u_lb[i] = d.u_lb[i];
     hp.u_ub[i] = d.u_ub[i];
@@ -2241,9 +2808,16 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
               const double* J, const double* b, const double* T, const double* mask, double* tau,
               double* x, int32_t* status, int32_t* iters, double* ws, double* warm, hipStream_t s,
               unsigned stages) {
-  if (stages & kAssemble)
-    hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
-                       model->dparams, nenv, M, C, J, b, T, mask, ws);
+  if (stages & kAssemble) {
+    // four envs per wavefront where its LDS fits (Go2), else one env per wavefront
+    if constexpr (OSC_SETUP4 && setup4_fits<D>())
+      hipLaunchKernelGGL(osc_setup4_kernel<D>,
+                         dim3(static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave)),
+                         dim3(kWave), 0, s, model->dparams, nenv, M, C, J, b, T, mask, ws);
+    else
+      hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0,
+                         s, model->dparams, nenv, M, C, J, b, T, mask, ws);
+  }
   if (stages & kInteriorPoint) {
     // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one
     // wave per SIMD, Hr in LDS where it fits); otherwise the two-waves-per-SIMD variant.
@@ -2367,8 +2941,18 @@ void launch_pair(const osc_batch_job& a, const osc_batch_job& b, hipStream_t s) 
     return p;
   };
   const PairArgs A = args(a), B = args(b);
-  hipLaunchKernelGGL((osc_setup_pair_kernel<DA, DB>), dim3(static_cast<unsigned>(a.nenv + b.nenv)),
-                     dim3(kWave), 0, s, A, B);
+  if constexpr (OSC_SETUP4 && setup4_fits<DB>() && !setup4_fits<DA>()) {
+    // model B's setup runs four envs per wavefront (its solo launch): the models' setups are two
+    // grids, so each model's reduced QP is bitwise the one of its solo solve
+    hipLaunchKernelGGL(osc_setup_kernel<DA>, dim3(static_cast<unsigned>(a.nenv)), dim3(kWave), 0, s,
+                       A.P, A.nenv, A.M, A.C, A.J, A.b, A.T, A.mask, A.ws);
+    hipLaunchKernelGGL(osc_setup4_kernel<DB>,
+                       dim3(static_cast<unsigned>((b.nenv + kEnvPerWave - 1) / kEnvPerWave)),
+                       dim3(kWave), 0, s, B.P, B.nenv, B.M, B.C, B.J, B.b, B.T, B.mask, B.ws);
+  } else {
+    hipLaunchKernelGGL((osc_setup_pair_kernel<DA, DB>),
+                       dim3(static_cast<unsigned>(a.nenv + b.nenv)), dim3(kWave), 0, s, A, B);
+  }
   const unsigned nb = static_cast<unsigned>((a.nenv + kEnvPerWave - 1) / kEnvPerWave +
                                             (b.nenv + kEnvPerWave - 1) / kEnvPerWave);
   // one-wave interior point of both models with the refinement in the same wavefront

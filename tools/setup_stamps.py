@@ -1,5 +1,6 @@
 """Diagnostic: per-phase cycles of the setup kernel from the OSC_STAMPS build
-(lib/libosc_batch_stamps.so): mean over waves (one env each) and the slowest wave.
+(lib/libosc_batch_stamps.so, or $OSC_STAMPS_LIB): mean over waves and the slowest wave
+(OSC_SETUP4=1: the four-envs-per-wave kernel, Go2).
     python tools/setup_stamps.py [nenv]"""
 import ctypes
 import json
@@ -7,7 +8,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["OSC_LIB_PATH"] = os.path.join(REPO, "operational-space-control_amd", "lib",
+os.environ["OSC_LIB_PATH"] = os.environ.get("OSC_STAMPS_LIB") or os.path.join(REPO, "operational-space-control_amd", "lib",
                                           "libosc_batch_stamps.so")
 sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
 import numpy as np  # noqa: E402
@@ -16,8 +17,10 @@ from osc_amd import _lib  # noqa: E402
 from osc_amd.solver import OSCBatchSolver  # noqa: E402
 from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
-NAMES = ["A: stage inputs", "B: Ha = 2[J e]'W[J e]", "C: X, U (base block)", "D1: T1",
-         "D2: Hr | g", "write workspace", "C2 (TY): factor S", "C2: solve", "C2: x_b + write"]
+NAMES = (["stage", "Ha", "X_b, U", "Schur + x", "X, H_dv -> ws", "T1", "Hr tiles", "g | Hr put"]
+         if os.environ.get("OSC_SETUP4") else
+         ["A: stage inputs", "B: Ha = 2[J e]'W[J e]", "C: X, U (base block)", "D1: T1",
+          "D2: Hr | g", "write workspace", "C2 (TY): factor S", "C2: solve", "C2: x_b + write"])
 SLOTS = 12
 nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 for robot in ["unitree_go2", "walter_sr"]:
@@ -28,11 +31,12 @@ for robot in ["unitree_go2", "walter_sr"]:
     for _ in range(2):
         s.assemble_into(out, *args)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (nenv * SLOTS))()
+    nw = nenv // 4 if os.environ.get("OSC_SETUP4") and robot == "unitree_go2" else nenv
+    buf = (ctypes.c_ulonglong * (nw * SLOTS))()
     L = _lib.lib()
     L.osc_debug_setup_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    assert L.osc_debug_setup_stamps(ctypes.cast(buf, ctypes.c_void_p), nenv) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(nenv, SLOTS)[:, :len(NAMES)].astype(np.float64)
+    assert L.osc_debug_setup_stamps(ctypes.cast(buf, ctypes.c_void_p), nw) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, SLOTS)[:, :len(NAMES)].astype(np.float64)
     tot = a.sum(axis=1)
     print(json.dumps({"robot": robot, "nenv": nenv, "mean_cycles": round(float(tot.mean())),
                       "max_cycles": round(float(tot.max())),
