@@ -401,6 +401,9 @@ def parse_args(argv=None):
     ap.add_argument("--single-env-ticks", type=int, default=2000)
     ap.add_argument("--no-pipeline", action="store_true",
                     help="walter_sr tumbling: skip the whole-tick device pipeline timing")
+    ap.add_argument("--event-every", type=int, default=5,
+                    help="HIP events around the two kernels on every N-th timed step (kernel "
+                         "durations for the roofline objects); the other steps run bare")
     ap.add_argument("--mask-redraw", type=int, default=0,
                     help="cycle through this many Bernoulli masks, one per step (configs[3]: "
                          "contact-mode switching, walter_sr_true_tumbling_mjjoint.cc:554-614)")
@@ -460,24 +463,31 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
     clock.sync()
 
     # Each step = osc_batch_assemble (setup kernel) + osc_batch_solve_assembled (interior-point
-    # kernel), the two halves of osc_batch_solve, with HIP events on the launch stream around
-    # each kernel.
-    ev = [[clock.event() for _ in range(3)] for _ in range(args.steps)]
+    # kernel), the two halves of osc_batch_solve.  HIP events on the launch stream around each
+    # kernel on every `event_every`-th step of the timed region (each event costs the stream ~3 us,
+    # tools/event_overhead.py: three per step were ~5 % of a Go2 4,096 step).
+    every = max(1, args.event_every)
+    sampled = [k for k in range(args.steps) if k % every == 0]
+    ev = {k: [clock.event() for _ in range(3)] for k in sampled}
     barrier()
     clock.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         mask = masks[k % len(masks)]
-        ev[k][0].record(stream)
+        e = ev.get(k)
+        if e:
+            e[0].record(stream)
         solver.assemble_into(out, *inputs[:5], mask)
-        ev[k][1].record(stream)
+        if e:
+            e[1].record(stream)
         solver.solve_assembled_into(out, mask)
-        ev[k][2].record(stream)
+        if e:
+            e[2].record(stream)
     clock.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev.values()) / len(ev)
+    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev.values()) / len(ev)
 
     st = out.status.cpu().numpy()
     mean_iters = float(out.iters.double().mean().item())
@@ -522,6 +532,9 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
+                     "kernel_ms_from": f"HIP events around the kernel on every "
+                                       f"{max(1, args.event_every)}-th timed step; batches "
+                                       f"past one wave per SIMD add osc_refine_kernel",
                      "bytes_per_solve": bps,
                      "inputs": "cache-warm: the same batch every step (its 31 MB stays in the "
                                "256 MB Infinity Cache); the kernel is latency-bound",

@@ -17,7 +17,8 @@ from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
 NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble: contact blocks", "LDL^T",
          "rhs (2 passes)", "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update",
-         "assemble: rd = g + G'lam + Hr y", "assemble: rank-1 U terms", "-", "-"]
+         "assemble: rd = g + G'lam + Hr y", "assemble: rank-1 U terms",
+         "refine: K_A + LDL", "refine: steps"]
 for robot in ["unitree_go2", "walter_sr"]:
     nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     s = OSCBatchSolver(robot)
@@ -31,11 +32,22 @@ for robot in ["unitree_go2", "walter_sr"]:
     L = _lib.lib()
     L.osc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.osc_debug_stamps(ctypes.cast(buf, ctypes.c_void_p), nblk) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, len(NAMES)).astype(np.float64)
+    raw = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, len(NAMES)).copy()
+    rounds = (raw[:, 10] >> np.uint64(40)).astype(np.int64)   # refinement rounds per wave
+    raw[:, 10] &= np.uint64((1 << 40) - 1)
+    a = raw.astype(np.float64)
     it = out.iters.cpu().numpy().reshape(nblk, 4).max(axis=1) + 1   # + init pass
     tot = a.sum(axis=1)
+    ipm = a[:, :10].sum(axis=1)
     per = {n: float(a[:, k].mean()) for k, n in enumerate(NAMES)}
+    slow = int(np.argmax(tot))
     print(json.dumps({"robot": robot, "mean_cycles_per_wave": float(tot.mean()),
                       "mean_wave_iters": float(it.mean()),
-                      "cycles_per_wave_iter": float((tot / it).mean()),
+                      "cycles_per_wave_iter": float((ipm / it).mean()),
+                      "refine_rounds_hist": np.bincount(rounds).tolist(),
+                      "slowest_wave": {"cycles": float(tot[slow]), "iters": int(it[slow]),
+                                       "refine_rounds": int(rounds[slow]),
+                                       "refine_cycles": float(a[slow, 10] + a[slow, 11])},
+                      "refine_cycles_per_round": float((a[:, 10] + a[:, 11]).sum() /
+                                                       max(rounds.sum(), 1)),
                       "share": {n: round(per[n] / tot.mean(), 3) for n in NAMES}}), flush=True)
