@@ -2322,7 +2322,9 @@ __device__ __forceinline__ void ipm_block(
     wave_sync();
     STAMP_END(7);
   }
-  STAMP_STORE();
+#ifdef OSC_STAMPS
+  if constexpr (RF != kRfFused) STAMP_STORE();   // the fused pass stores after its refinement
+#endif
   if constexpr (D::TY && RF == kRfNone) {   // hand the result to the refinement kernel
     if (write_out) {
       // (the W_SOL block is written here and read by nothing else in this kernel)
@@ -2380,6 +2382,10 @@ __device__ __forceinline__ void ipm_block(
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
       for (int round = 0; round < 3; ++round) {
+        STAMP_BEGIN();
+#ifdef OSC_STAMPS
+        st_acc[10] += 1ull << 40;   // rounds, in the top bits of the assembly+LDL slot
+#endif
         if (round > 0) {   // c0 / c1 hold the last round's factor
           if constexpr (kXinHr) {
             // Hr's LDS region holds X now: Hr columns from the (L2-resident) workspace
@@ -2442,6 +2448,8 @@ __device__ __forceinline__ void ipm_block(
         wave_sync();
         ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
         wave_sync();
+        STAMP_END(10);
+        STAMP_BEGIN();
         for (int k = 0; k < P->refine_steps; ++k) {
           // dv = X [y; 1] (rows l, l + 16) -> sXb
 #pragma unroll
@@ -2521,6 +2529,7 @@ __device__ __forceinline__ void ipm_block(
           nviol += v ? 1.0 : 0.0;
         }
         viol_env = mine && row_max(nviol) > 0.0;
+        STAMP_END(11);
         if (__ballot(viol_env) == 0) break;
       }
       // keep the refined iterate when it is feasible, finite and close to the interior point's
@@ -2540,6 +2549,9 @@ __device__ __forceinline__ void ipm_block(
     }
   }
 
+#ifdef OSC_STAMPS
+  if constexpr (RF == kRfFused) STAMP_STORE();
+#endif
   // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
   if (REFINE && !refined) write_out = false;   // the interior point kernel's outputs stand
   if (l < NU) {
