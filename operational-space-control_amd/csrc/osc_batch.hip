@@ -1718,6 +1718,17 @@ __device__ __forceinline__ void ipm_block(
     Batch2<LY::STAGE / 2, kRow> bs;
     bs.load(ws + static_cast<size_t>(env) * D::WS, l);
     const double mk = gmask[static_cast<size_t>(env) * NC + (l < NC ? l : 0)];
+    if constexpr (RF == kRfFused) {
+      // the refinement's own LDS block is free all along: its [X | H_dv | f_dv] (HRL:
+      // [H_dv | f_dv]; X takes Hr's region later) is staged now, in the same memory latency
+      // (by DMA instead, the allocator spills the one-wave Go2 kernel to scratch)
+      constexpr int kFrom = kXinHr ? RefineLds<D>::HD : 0;
+      static_assert((RefineLds<D>::SIZE - kFrom) % 2 == 0 && (D::W_X + kFrom) % 2 == 0,
+                    "16-byte staging");
+      Batch2<(RefineLds<D>::SIZE - kFrom) / 2, kRow> bx;
+      bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X + kFrom, l);
+      bx.store(kXinHr ? sRH : sRX, l);
+    }
     bs.store(B, l);
     if (l < NC) sMask[l] = mk;
   }
@@ -2369,15 +2380,6 @@ __device__ __forceinline__ void ipm_block(
       double ya0 = y0, ya1 = y1;
       bool viol_env = false;
       const double* wenv = ws + static_cast<size_t>(env) * D::WS;
-      if constexpr (RF == kRfFused) {
-        // this env's [X | H_dv | f_dv] (HRL: [H_dv | f_dv]; X follows once Hr's region is free)
-        constexpr int kFrom = kXinHr ? RefineLds<D>::HD : 0;
-        static_assert((RefineLds<D>::SIZE - kFrom) % 2 == 0 && (D::W_X + kFrom) % 2 == 0,
-                      "16-byte staging");
-        Batch2<(RefineLds<D>::SIZE - kFrom) / 2, kRow> bx;
-        bx.load(wenv + D::W_X + kFrom, l);
-        bx.store(kXinHr ? sRH : sRX, l);
-      }
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
@@ -2436,19 +2438,43 @@ __device__ __forceinline__ void ipm_block(
             c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
           }
         }
+        // HRL: X is copied global -> LDS by DMA (no registers) into Hr's region -- free now, K_A
+        // is in registers -- issued before the factorisation, waited for after it, so its latency
+        // hides behind the LDL^T.  A DMA wave-instruction writes 16 B per lane to a wave-uniform
+        // base + 16 B x lane, so each one fills 1 KB of ONE env's block with all 64 lanes (every
+        // lane loads that env's chunk): compile-time bases, no per-env branches.
         if constexpr (kXinHr) {
-          if (round == 0) {   // K_A is in registers: X takes Hr's region
-            static_assert(D::NV * D::NY1P <= even(NY * NY) && D::W_X % 2 == 0, "X in Hr's region");
-            Batch2<D::NV * D::NY1P / 2, kRow> bx;
-            bx.load(wenv + D::W_X, l);
-            wave_sync();   // every lane's Hr reads (load_hr) are done
-            bx.store(sRX, l);
+          constexpr int NCH = D::NV * D::NY1P / 2;               // 16-byte chunks of X
+          constexpr int NT = (NCH + kWave - 1) / kWave;
+          static_assert(D::NV * D::NY1P <= even(NY * NY) && D::W_X % 2 == 0 &&
+                        NT * kWave * 2 <= even(NY * NY), "X (whole DMA rows) in Hr's region");
+          if (round == 0) {
+            static_for<0, kEnvPerWave>([&](auto G) {
+              constexpr int g = decltype(G)::value;
+              const int eg = blk * kEnvPerWave + g < nenv ? blk * kEnvPerWave + g : nenv - 1;
+              const double2* src =
+                  reinterpret_cast<const double2*>(ws + static_cast<size_t>(eg) * D::WS + D::W_X);
+              static_for<0, NT>([&](auto T) {
+                constexpr int t = decltype(T)::value;
+                const int c = lane + kWave * t < NCH ? lane + kWave * t : NCH - 1;
+#if defined(__HIP_DEVICE_COMPILE__)   // (a device builtin: the host pass never runs this body)
+                __builtin_amdgcn_global_load_lds(src + c, sm + g * kEnvLds + LY::I_HR + 2 * kWave * t,
+                                                 16, 0, 0);
+#else
+                (void)src;
+                (void)c;
+#endif
+              });
+            });
           }
         }
         wave_sync();
         ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+        if constexpr (kXinHr) {
+          if (round == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X has landed
+        }
         wave_sync();
-        STAMP_END(10);
+        STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
         for (int k = 0; k < P->refine_steps; ++k) {
           // dv = X [y; 1] (rows l, l + 16) -> sXb
