@@ -467,7 +467,8 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
     # kernel on every `event_every`-th step of the timed region (each event costs the stream ~3 us,
     # tools/event_overhead.py: three per step were ~5 % of a Go2 4,096 step).
     every = max(1, args.event_every)
-    sampled = [k for k in range(args.steps) if k % every == 0]
+    # (the last step of each group of `every`: steady state, not the first launch after the barrier)
+    sampled = [k for k in range(args.steps) if k % every == every - 1] or [args.steps - 1]
     ev = {k: [clock.event() for _ in range(3)] for k in sampled}
     barrier()
     clock.sync()
