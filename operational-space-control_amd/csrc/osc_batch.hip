@@ -80,6 +80,15 @@ constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regio
 // TY_ selects the reduced coordinates: false -> y = (dv_a, z), u = U [y; 1] (dense torque rows,
 // only the base block M_bb is inverted); true -> y = (u, z), dv = X [y; 1] = M^-1 (B u + Jc z - C)
 // over all nv rows, so the torque bounds are plain bounds on y (diagonal in the Newton matrix).
+// Assembly products on the FP64 matrix cores (torque-coordinate models): bit 0 = T1 and Hr
+// (phase D), bit 1 = Ha (phase B) for every model (by default only where NA <= 16); 0 = VALU
+// 2x2 tiles everywhere.  FP64 MFMA has the FP64 VALU's
+// peak on gfx950 (tools/mb_mfma64.hip: ~70 clocks per 16x16x4), so it only pays where it saves
+// LDS round trips: phase D keeps T1 in registers; Ha's padded 16x16 tiles (19 -> 32) cost more
+// than the VALU's exact 2x2 tiles (Go2 4,096: phase B 7.7k vs 3.5k clocks per wave)
+#ifndef OSC_SETUP_MFMA
+#define OSC_SETUP_MFMA 1
+#endif
 template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
@@ -133,11 +142,12 @@ struct Dims {
   static constexpr int NBT = (NV / 2) * NY2;             // T1 tiles
   static constexpr int NBH = NY2 * (NY2 + 1) / 2;        // Hr | g tiles (upper triangle)
   static constexpr int R1_A = S * NAP;                                  // A = [J | e | 0]
-  static constexpr int R1_D = NV * NY1P + even(NY * NY);                // T1 | Hr
+  static constexpr bool MF = (OSC_SETUP_MFMA & 1) && TY;   // MFMA products: T1 stays in registers
+  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + even(NY * NY);     // (T1 |) Hr
   static constexpr int R1 = cmax(R1_A, R1_D);
   static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
   static constexpr int O_A = 0;
-  static constexpr int O_T1 = 0, O_HR = NV * NY1P;
+  static constexpr int O_T1 = 0, O_HR = MF ? 0 : NV * NY1P;
   static constexpr int O_M = R1, O_C = R1 + even(NV * NV), O_G = R1;
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
@@ -447,6 +457,17 @@ __device__ __forceinline__ double bcast_guarded(double v) {
 }
 
 // ============================ kernel 1: reduced QP per env ==================================
+// Dense products of the assembly (2 A'WA, H_dv X, X'(H_dv X)) on the FP64 matrix cores
+// (v_mfma_f64_16x16x4f64) for torque-coordinate models; OSC_SETUP_MFMA=0 builds the VALU 2x2-tile
+// form for A/B.
+typedef double d4 __attribute__((ext_vector_type(4)));
+template <class D>
+constexpr bool kSetupMfma = D::MF;
+// Ha on MFMA: forced by bit 1, else where [J e] fits one 16-column block (WaLTER: NA = 15, one
+// tile over 102 task rows, phase B 10.9k -> 8.9k clocks per wave; Go2's NA = 19 pads to 32)
+template <class D>
+constexpr bool kHaMfma = D::TY && ((OSC_SETUP_MFMA & 2) || ((OSC_SETUP_MFMA & 1) && D::NA <= 16));
+
 // The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
 // of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
 // grid: BASELINE configs[4]).
@@ -521,6 +542,55 @@ __device__ __forceinline__ void setup_env(
     sHa[i * NA + j] = v;
     sHa[j * NA + i] = v;
   };
+  if constexpr (kHaMfma<D>) {
+    // FP64 MFMA (v_mfma_f64_16x16x4f64): 16x16 tiles of the upper block triangle, K = task rows
+    // in steps of 4.  Lane l feeds row/column (l & 15) of a block at k-row 4q + (l >> 4) and
+    // gets back C[(l >> 4) + 4 r][l & 15] (tools/mb_mfma64.hip checks this layout on the GPU).
+    // Only entries i <= j are stored (then mirrored): H_dv is exactly symmetric.
+    constexpr int NBK = (NA + 15) / 16, KS = (S + 3) / 4;
+    const int lc = lane & 15, lg = lane >> 4;
+    d4 acc[NBK * (NBK + 1) / 2];
+#pragma unroll
+    for (int t = 0; t < NBK * (NBK + 1) / 2; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    // fragments of CH k-steps loaded together (row weights included), then their MFMAs: one
+    // memory latency per chunk instead of one per k-step
+    constexpr int CH = 8;
+    for (int q0 = 0; q0 < KS; q0 += CH) {
+      double v[CH][NBK], wv[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int r = 4 * (q0 + u) + lg;
+        const bool rv = r < S;
+        wv[u] = rv ? P->w_row[rv ? r : 0] : 0.0;
+#pragma unroll
+        for (int b = 0; b < NBK; ++b) {
+          const int col = 16 * b + lc;
+          const double x = sA[(rv ? r : 0) * NAP + (col < NAP ? col : 0)];
+          v[u][b] = (rv && col < NAP) ? x : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (q0 + u >= KS) break;
+        int t = 0;
+#pragma unroll
+        for (int bi = 0; bi < NBK; ++bi)
+#pragma unroll
+          for (int bj = bi; bj < NBK; ++bj, ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(wv[u] * v[u][bi], v[u][bj], acc[t], 0, 0, 0);
+      }
+    }
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NBK; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < NBK; ++bj, ++t)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int i = 16 * bi + lg + 4 * rr, j = 16 * bj + lc;
+          if (i <= j) put_ha(i, j, acc[t][rr]);
+        }
+  } else
   for (int p = lane; p < D::NBA; p += kWave) {
     int i0, j0;
     upper_pair<D::NA2>(p, i0, j0);
@@ -737,6 +807,93 @@ __device__ __forceinline__ void setup_env(
       return (c < NU || c == NY) ? v : 0.0;
     }
   };
+  if constexpr (kSetupMfma<D>) {
+    // FP64 MFMA, torque coordinates: T1 = H_dv X (+ f_dv in the affine column) as 16x16 tiles
+    // kept in registers, then [Hr | g] = X' T1 with T1's registers as the B operand -- register
+    // r of a T1 tile holds rows (l >> 4) + 4 r, exactly the k-rows of one 4-step -- so T1 never
+    // goes through LDS.  X's fragments serve both products (B of the first, A of the second).
+    static_assert(D::TY && D::NXR == NV, "MFMA setup: torque coordinates");
+    constexpr int RB = (NV + 15) / 16, CB = (NY1P + 15) / 16, KS = (NV + 3) / 4;
+    const int lc = lane & 15, lg = lane >> 4;
+    double xf[KS][CB];   // X[4q + lg][16 cb + lc]
+    double hf[RB][KS];   // H_dv[16 rb + lc][4q + lg]
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int k = 4 * q + lg;
+      const bool kv = k < NV;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        const int col = 16 * cb + lc;
+        const double x = sX[(kv ? k : 0) * NY1P + (col < NY1P ? col : 0)];
+        xf[q][cb] = (kv && col < NY1P) ? x : 0.0;
+      }
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const int row = 16 * rb + lc;
+        const double h = sHa[(row < NV ? row : 0) * NA + (kv ? k : 0)];
+        hf[rb][q] = (kv && row < NV) ? h : 0.0;
+      }
+    }
+    d4 t1[RB][CB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = 16 * rb + lg + 4 * rr, col = 16 * cb + lc;
+          const double f = sHa[(row < NV ? row : 0) * NA + NV];
+          t1[rb][cb][rr] = (row < NV && col == NY) ? f : 0.0;
+        }
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          t1[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(hf[rb][q], xf[q][cb], t1[rb][cb], 0, 0, 0);
+    const double wu2 = 2.0 * (P->w_torque + P->w_reg);
+    const double wr2 = 2.0 * P->w_reg;
+    constexpr int NT = CB * (CB + 1) / 2;   // upper block triangle, tiles interleaved per k-step
+    d4 hacc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) hacc[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      int t = 0;
+#pragma unroll
+      for (int ab = 0; ab < CB; ++ab)
+#pragma unroll
+        for (int bb = ab; bb < CB; ++bb, ++t)
+          hacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xf[q][ab], t1[q / 4][bb][q % 4], hacc[t],
+                                                         0, 0, 0);
+    }
+    int tt = 0;
+#pragma unroll
+    for (int ab = 0; ab < CB; ++ab)
+#pragma unroll
+      for (int bb = ab; bb < CB; ++bb, ++tt) {
+        const d4 h = hacc[tt];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int a = 16 * ab + lg + 4 * rr, b = 16 * bb + lc;
+          const int kz = (a >= NU) ? (a - NU) / 3 : 0;
+          const double mk = sMask[kz < NC ? kz : NC - 1];
+          double v = h[rr];
+          if (a <= b && b < NY1 && !(a == NY && b == NY)) {
+            if (b < NY) {
+              if (a == b && a < NU) v += wu2;
+              if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
+              sHr[a * NY + b] = v;
+              sHr[b * NY + a] = v;
+            } else {
+              sG[a] = v;
+            }
+          }
+        }
+      }
+    wave_sync();
+  } else {
   for (int p = lane; p < D::NBT; p += kWave) {
     const int r0 = 2 * (p / D::NY2), c0 = 2 * (p % D::NY2);
     double t00 = t1_base(r0, c0), t01 = t1_base(r0, c0 + 1);
@@ -817,6 +974,7 @@ __device__ __forceinline__ void setup_env(
     }
   }
   wave_sync();
+  }
 
   STAMP_END(4);
   STAMP_BEGIN();
