@@ -141,9 +141,18 @@ struct Dims {
   static constexpr int NBA = NA2 * (NA2 + 1) / 2;        // Ha tiles (upper triangle)
   static constexpr int NBT = (NV / 2) * NY2;             // T1 tiles
   static constexpr int NBH = NY2 * (NY2 + 1) / 2;        // Hr | g tiles (upper triangle)
-  static constexpr int R1_A = S * NAP;                                  // A = [J | e | 0]
   static constexpr bool MF = (OSC_SETUP_MFMA & 1) && TY;   // MFMA products: T1 stays in registers
-  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + even(NY * NY);     // (T1 |) Hr
+  // Ha on MFMA (forced by bit 1, else where [J e] fits one 16-column tile: WaLTER, NA = 15)
+  static constexpr bool HAM = TY && ((OSC_SETUP_MFMA & 2) || ((OSC_SETUP_MFMA & 1) && NA <= 16));
+  // J not staged: Ha's MFMA fragments come straight from global memory, LDS holds only the
+  // contact rows phase C reads (WaLTER: 102 x 16 -> 24 x 16 doubles), and [Hr | g] go to the
+  // workspace from phase D's registers (no LDS copy): setup LDS 20.4 -> 10.4 KB.  (Go2 keeps the
+  // LDS copy of Hr: the register-direct stores took its VGPRs from 108 to the 252 cap.)
+  static constexpr bool JG = HAM && MF;
+  static constexpr int JROWS = JG ? 3 * NC : S;                         // rows of A in LDS
+  static constexpr int R1_A = JROWS * NAP + (JG ? 2 * even(S) : 0);    // A = [J | e | 0] (| e | w)
+  static constexpr int O_E = JROWS * NAP, O_W = O_E + even(S);          // JG: e = b - t, row weights
+  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + (JG ? 0 : even(NY * NY));   // (T1 |) Hr
   static constexpr int R1 = cmax(R1_A, R1_D);
   static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
   static constexpr int O_A = 0;
@@ -466,7 +475,7 @@ constexpr bool kSetupMfma = D::MF;
 // Ha on MFMA: forced by bit 1, else where [J e] fits one 16-column block (WaLTER: NA = 15, one
 // tile over 102 task rows, phase B 10.9k -> 8.9k clocks per wave; Go2's NA = 19 pads to 32)
 template <class D>
-constexpr bool kHaMfma = D::TY && ((OSC_SETUP_MFMA & 2) || ((OSC_SETUP_MFMA & 1) && D::NA <= 16));
+constexpr bool kHaMfma = D::HAM;
 
 // The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
 // of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
@@ -499,17 +508,41 @@ __device__ __forceinline__ void setup_env(
   // ---------------- Phase A: stage this env's inputs HBM -> LDS ----------------
   // every load first (one memory latency), then the LDS stores
   static_assert(NV % 2 == 0 && NC % 2 == 0, "16-byte staging needs even nv and nc");
-  Batch2<S * NV / 2, kWave> bJ;
+  constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
+  constexpr int JR0 = D::JG ? JC0 : 0; // first row of J staged (JG: the contact rows only)
+  Batch2<D::JROWS * NV / 2, kWave> bJ;
   Batch2<NV * NV / 2, kWave> bM;
   Batch2<NV / 2, kWave> bC;
   Batch2<NC / 2, kWave> bK;
-  bJ.load(gJ + static_cast<size_t>(env) * S * NV, lane);
+  bJ.load(gJ + static_cast<size_t>(env) * S * NV + JR0 * NV, lane);
   bM.load(gM + static_cast<size_t>(env) * NV * NV, lane);
   bC.load(gC + static_cast<size_t>(env) * NV, lane);
   bK.load(gmask + static_cast<size_t>(env) * NC, lane);
+  // JG: phase B's MFMA fragments of J (row 4q + (lane >> 4), column lane & 15) loaded now, in the
+  // same memory latency as the staging loads; e and the row weights go to LDS
+  constexpr int KSJ = D::JG ? (S + 3) / 4 : 0;
+  double jf[KSJ > 0 ? KSJ : 1];
+  {
+    const int lc = lane & 15, lg = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < KSJ; ++q) {
+      const int r = 4 * q + lg;
+      jf[q] = gJ[static_cast<size_t>(env) * S * NV + (r < S ? r : S - 1) * NV + (lc < NV ? lc : 0)];
+    }
+  }
+  constexpr int TEJ = D::JG ? (S + kWave - 1) / kWave : 0;
+  double ebj[TEJ > 0 ? TEJ : 1], etj[TEJ > 0 ? TEJ : 1], wj[TEJ > 0 ? TEJ : 1];
+#pragma unroll
+  for (int q = 0; q < TEJ; ++q) {
+    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+    const int half = r / (3 * NS), rr = r % (3 * NS);
+    ebj[q] = gb[static_cast<size_t>(env) * S + r];
+    etj[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+    wj[q] = P->w_row[r];
+  }
   // A column NV: e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168)
-  constexpr int TE = (S + kWave - 1) / kWave;
-  double eb[TE], et[TE];
+  constexpr int TE = D::JG ? 0 : (S + kWave - 1) / kWave;   // (JG: e enters phase B's fragments)
+  double eb[TE > 0 ? TE : 1], et[TE > 0 ? TE : 1];
 #pragma unroll
   for (int q = 0; q < TE; ++q) {
     const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
@@ -518,6 +551,12 @@ __device__ __forceinline__ void setup_env(
     et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
   }
   bJ.store(sA, lane, [](int c) { return (c / (NV / 2)) * (NAP / 2) + c % (NV / 2); });   // J rows -> A rows
+#pragma unroll
+  for (int q = 0; q < TEJ; ++q) {
+    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+    sA[D::O_E + r] = ebj[q] - etj[q];
+    sA[D::O_W + r] = wj[q];
+  }
   bM.store(sM, lane);
   bC.store(sC, lane);
   bK.store(sMask, lane);
@@ -555,18 +594,25 @@ __device__ __forceinline__ void setup_env(
     // fragments of CH k-steps loaded together (row weights included), then their MFMAs: one
     // memory latency per chunk instead of one per k-step
     constexpr int CH = 8;
+#pragma unroll   // (compile-time k-steps: JG indexes the register fragments jf by them)
     for (int q0 = 0; q0 < KS; q0 += CH) {
       double v[CH][NBK], wv[CH];
 #pragma unroll
       for (int u = 0; u < CH; ++u) {
         const int r = 4 * (q0 + u) + lg;
         const bool rv = r < S;
-        wv[u] = rv ? P->w_row[rv ? r : 0] : 0.0;
+        wv[u] = rv ? (D::JG ? sA[D::O_W + r] : P->w_row[r]) : 0.0;
 #pragma unroll
         for (int b = 0; b < NBK; ++b) {
           const int col = 16 * b + lc;
-          const double x = sA[(rv ? r : 0) * NAP + (col < NAP ? col : 0)];
-          v[u][b] = (rv && col < NAP) ? x : 0.0;
+          if constexpr (D::JG) {
+            // [J | e | 0] row r: J from the fragments loaded in phase A, e from LDS
+            const double ev = sA[D::O_E + (rv ? r : 0)];
+            v[u][b] = !rv ? 0.0 : (col < NV ? jf[q0 + u < KSJ ? q0 + u : 0] : (col == NV ? ev : 0.0));
+          } else {
+            const double x = sA[(rv ? r : 0) * NAP + (col < NAP ? col : 0)];
+            v[u][b] = (rv && col < NAP) ? x : 0.0;
+          }
         }
       }
 #pragma unroll
@@ -618,7 +664,6 @@ __device__ __forceinline__ void setup_env(
   // ---------------- Phase C: base-block elimination  X = M_bb^-1 [-M_ba | Jc_b | -C_b] -------
   // and the torque map U = M_a Pm + [M_aa | -Jc_a | C_a]  so that  u = U [y; 1].
   // (dynamics rows: autogen.py:58-89; Jc = Jp[last 3nc rows]^T: osc.h:439-445)
-  constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
   // One lane per column c of [y; 1]; when two copies of the 32-lane column set fit the wave,
   // both halves solve for X (redundantly) and split the NU rows of U between them.
   constexpr bool kSplitU = 2 * NY1P <= kWave;
@@ -633,10 +678,11 @@ __device__ __forceinline__ void setup_env(
     //   c < NY : Jc_b column,     U0 = -Jc_a column        (row JC0 + c - NU of A)
     //   c = NY : -C_b,            U0 = C_a
     const bool cu = c < NU, cz = !cu && c < NY;
-    const double* xp = cu ? sM + NB + c : (cz ? sA + (JC0 + c - NU) * NAP : sC);
+    const double* xp = cu ? sM + NB + c : (cz ? sA + (JC0 - JR0 + c - NU) * NAP : sC);
     const int xs = cu ? NV : 1;
     const double xsg = cz ? 1.0 : -1.0;
-    const double* up = cu ? sM + NB * NV + NB + c : (cz ? sA + (JC0 + c - NU) * NAP + NB : sC + NB);
+    const double* up =
+        cu ? sM + NB * NV + NB + c : (cz ? sA + (JC0 - JR0 + c - NU) * NAP + NB : sC + NB);
     const double usg = cz ? -1.0 : 1.0;
     double x[NB];
 #pragma unroll
@@ -854,6 +900,7 @@ __device__ __forceinline__ void setup_env(
           t1[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(hf[rb][q], xf[q][cb], t1[rb][cb], 0, 0, 0);
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
+    double* wsv = ws + static_cast<size_t>(env) * D::WS;   // JG: [Hr | g] out from registers
     constexpr int NT = CB * (CB + 1) / 2;   // upper block triangle, tiles interleaved per k-step
     d4 hacc[NT];
 #pragma unroll
@@ -884,10 +931,16 @@ __device__ __forceinline__ void setup_env(
             if (b < NY) {
               if (a == b && a < NU) v += wu2;
               if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
-              sHr[a * NY + b] = v;
-              sHr[b * NY + a] = v;
+              if constexpr (D::JG) {
+                wsv[D::W_HR + a * NY + b] = v;
+                wsv[D::W_HR + b * NY + a] = v;
+              } else {
+                sHr[a * NY + b] = v;
+                sHr[b * NY + a] = v;
+              }
             } else {
-              sG[a] = v;
+              if constexpr (D::JG) wsv[D::W_G + a] = v;
+              else sG[a] = v;
             }
           }
         }
@@ -980,8 +1033,10 @@ __device__ __forceinline__ void setup_env(
   STAMP_BEGIN();
   // ---------------- write the reduced QP: workspace [Hr | g | U | X] -------------------------
   double* w = ws + static_cast<size_t>(env) * D::WS;
-  for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
-  for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
+  if constexpr (!D::JG) {   // (JG: written from phase D's registers)
+    for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
+    for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
+  }
   for (int i = lane; i < D::NUW * NY1P; i += kWave) w[D::W_U + i] = sU[i];
   for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
   if constexpr (D::TY) {
@@ -992,13 +1047,29 @@ __device__ __forceinline__ void setup_env(
   STAMP_STORE_SETUP();
 }
 
+// XCD-aware env order of the assembly grid.  Blocks are dealt round-robin over the 8 XCDs
+// (block b and b + 8 share one; MI355X_MICROARCH.md), and interior-point block w (envs 4w..4w+3)
+// runs on XCD w % 8, so setup block b takes an env of an interior-point block on its own XCD:
+// the reduced QP the interior point reads right after is then in that XCD's L2 rather than
+// another XCD's.  A bijection on [0, nenv) when nenv is a multiple of 32, identity otherwise.
+#ifndef OSC_SETUP_XCD
+#define OSC_SETUP_XCD 0   // A/B: no measurable change (Go2 4,096 0.1819 vs 0.1815 ms)
+#endif
+__device__ __forceinline__ int setup_env_of_block(int b, int nenv) {
+  if (!OSC_SETUP_XCD || (nenv & 31) != 0) return b;
+  const int x = b & 7, m = b >> 3;                  // XCD, index among its blocks
+  const int w = 8 * (m >> 2) + x;                   // interior-point block on XCD x
+  return 4 * w + (m & 3);
+}
+
 template <class D>
 __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
   __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
-  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm);
+  setup_env<D>(P, setup_env_of_block(static_cast<int>(blockIdx.x), nenv), nenv, gM, gC, gJ, gb, gT,
+               gmask, ws, sm);
 }
 
 // One model's arguments to a two-model launch.
