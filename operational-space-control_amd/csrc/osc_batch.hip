@@ -1862,6 +1862,9 @@ constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
 #ifndef OSC_FUSE_REFINE
 #define OSC_FUSE_REFINE 1
 #endif
+#ifndef OSC_HR_REG
+#define OSC_HR_REG 1
+#endif
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
@@ -2179,6 +2182,18 @@ __device__ __forceinline__ void ipm_block(
 
   double c0[NY], c1[NY];
   double dinv0, dinv1;
+  // One-wave variant whose Hr does not fit the LDS (WaLTER: 32 x 32 x 4 envs): the lane's two Hr
+  // columns are loaded once and kept in registers across the iterations (the one-wave kernel has
+  // 512 of them, AGPRs included) instead of being re-read from L2 every iteration.
+  constexpr bool kHrReg = SMALL && !HRL && OSC_HR_REG;
+  double hr0[kHrReg ? NY : 1], hr1[kHrReg ? NY : 1];
+  if constexpr (kHrReg) {
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      hr0[i] = wsw[lane_off + static_cast<unsigned>(i * NY + j0)];
+      hr1[i] = wsw[lane_off + static_cast<unsigned>(i * NY + jj1)];
+    }
+  }
   // Hr columns j0, j1 (and their diagonal entries) -> registers; re-issued at the end of every
   // iteration so the loads fly while the step is applied and the next residuals are formed.
   auto load_hr = [&]() {
@@ -2189,6 +2204,12 @@ __device__ __forceinline__ void ipm_block(
       for (int i = 0; i < NY; ++i) {
         c0[i] = sHr[i * NY + j0];
         c1[i] = sHr[i * NY + jj1];
+      }
+    } else if constexpr (kHrReg) {
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        c0[i] = hr0[i];
+        c1[i] = hr1[i];
       }
     } else {
       unsigned off = lane_off;
