@@ -1865,6 +1865,9 @@ constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
 #ifndef OSC_HR_REG
 #define OSC_HR_REG 1
 #endif
+#ifndef OSC_FUSE_REFINE_LARGE   // the two-wave variant runs the refinement too (no second kernel)
+#define OSC_FUSE_REFINE_LARGE 1
+#endif
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
@@ -1875,6 +1878,7 @@ constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's itera
 template <class D, bool SMALL, int RF>
 constexpr int refine_lds_extra() {
   if constexpr (RF == kRfNone || !D::TY) return 0;
+  else if constexpr (RF == kRfFused && !SMALL) return 0;   // reads [X | H_dv | f_dv] from L2
   else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())
     return RefineLds<D>::SIZE - RefineLds<D>::HD;
   else return RefineLds<D>::SIZE;
@@ -1923,6 +1927,10 @@ __device__ __forceinline__ void ipm_block(
   double* sRX = kXinHr ? B + LY::I_HR : B + LY::IL + RefineLds<D>::X;
   double* sRH = kXinHr ? B + LY::IL : B + LY::IL + RefineLds<D>::HD;
   double* sRG = sRH + (RefineLds<D>::GD - RefineLds<D>::HD);
+  // Two-wave variant with the refinement fused: no LDS for [X | H_dv | f_dv] (two waves per SIMD
+  // need <= 20 KB per wave), the refinement reads them from the workspace (L2 / Infinity Cache)
+  // (the pointers are formed after the interior-point loop: nothing extra lives across it)
+  constexpr bool kRefG = RF == kRfFused && !SMALL;
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -1950,7 +1958,7 @@ __device__ __forceinline__ void ipm_block(
     Batch2<LY::STAGE / 2, kRow> bs;
     bs.load(ws + static_cast<size_t>(env) * D::WS, l);
     const double mk = gmask[static_cast<size_t>(env) * NC + (l < NC ? l : 0)];
-    if constexpr (RF == kRfFused) {
+    if constexpr (RF == kRfFused && !kRefG) {
       // the refinement's own LDS block is free all along: its [X | H_dv | f_dv] (HRL:
       // [H_dv | f_dv]; X takes Hr's region later) is staged now, in the same memory latency
       // (by DMA instead, the allocator spills the one-wave Go2 kernel to scratch)
@@ -2630,6 +2638,10 @@ __device__ __forceinline__ void ipm_block(
       double ya0 = y0, ya1 = y1;
       bool viol_env = false;
       const double* wenv = ws + static_cast<size_t>(env) * D::WS;
+      const double* rX = kRefG ? wenv + D::W_X : sRX;
+      const double* rH = kRefG ? wenv + D::W_HD : sRH;
+      const double* rG = kRefG ? wenv + D::W_GD : sRG;
+      constexpr int kUr = kRefG ? 2 : 32;   // workspace reads: few in flight (registers)
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
@@ -2732,9 +2744,9 @@ __device__ __forceinline__ void ipm_block(
           for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
             const int rr = l + kRow * t;
             if (rr < NV) {
-              const double* xr = sRX + rr * NY1P;
+              const double* xr = rX + rr * NY1P;
               double a = xr[NY];
-#pragma unroll
+#pragma unroll(kUr)
               for (int i = 0; i < NY; ++i) a = fma(xr[i], sVy[i], a);
               sXb[rr] = a;
             }
@@ -2747,9 +2759,9 @@ __device__ __forceinline__ void ipm_block(
             const int rr = l + kRow * t;
             gxr[t] = 0.0;
             if (rr < NV) {
-              const double* hr = sRH + rr * NV;
-              double a = sRG[rr];
-#pragma unroll
+              const double* hr = rH + rr * NV;
+              double a = rG[rr];
+#pragma unroll(kUr)
               for (int i = 0; i < NV; ++i) a = fma(hr[i], sXb[i], a);
               gxr[t] = a;
             }
@@ -2763,10 +2775,10 @@ __device__ __forceinline__ void ipm_block(
           wave_sync();
           // r_j = X[:, j]' gx + diag_j y_j + (G_A' mu)_j for the lane's two variables
           double r0 = (j0 < NU ? wu : wz) * ya0, r1 = (jj1 < NU ? wu : wz) * ya1;
-#pragma unroll
+#pragma unroll(kUr)
           for (int i = 0; i < NV; ++i) {
-            r0 = fma(sRX[i * NY1P + j0], sDr[i], r0);
-            r1 = fma(sRX[i * NY1P + jj1], sDr[i], r1);
+            r0 = fma(rX[i * NY1P + j0], sDr[i], r0);
+            r1 = fma(rX[i * NY1P + jj1], sDr[i], r1);
           }
           double gm0, gm1;
           GTw2(sVr, gm0, gm1);
@@ -3117,10 +3129,14 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
       status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
     const bool small = nenv <= model->small_batch_max;
     // The one-wave cold solve runs the refinement in the same wavefront (kRfFused).
-    const bool fused = OSC_FUSE_REFINE && small && warm == nullptr && D::TY && model->refine;
+    const bool fused = OSC_FUSE_REFINE && (small || OSC_FUSE_REFINE_LARGE) && warm == nullptr &&
+                       D::TY && model->refine;
     if (warm == nullptr) {
-      if (fused)
+      if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+      else if (fused)
+        hipLaunchKernelGGL((osc_ipm_kernel<D, false, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
       else if (small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false>), dim3(nb), dim3(kWave), 0, s,
