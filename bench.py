@@ -534,8 +534,8 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
                      "kernel_ms_from": f"HIP events around the kernel on every "
-                                       f"{max(1, args.event_every)}-th timed step; batches "
-                                       f"past one wave per SIMD add osc_refine_kernel",
+                                       f"{max(1, args.event_every)}-th timed step (the "
+                                       f"full-space refinement runs inside it)",
                      "bytes_per_solve": bps,
                      "inputs": "cache-warm: the same batch every step (its 31 MB stays in the "
                                "256 MB Infinity Cache); the kernel is latency-bound",
