@@ -1868,6 +1868,9 @@ constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
 #ifndef OSC_FUSE_REFINE_LARGE   // the two-wave variant runs the refinement too (no second kernel)
 #define OSC_FUSE_REFINE_LARGE 1
 #endif
+#ifndef OSC_FUSE_REFINE_WARM    // so do the warm-started solve's two passes
+#define OSC_FUSE_REFINE_WARM 1
+#endif
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
@@ -3131,6 +3134,10 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     // The one-wave cold solve runs the refinement in the same wavefront (kRfFused).
     const bool fused = OSC_FUSE_REFINE && (small || OSC_FUSE_REFINE_LARGE) && warm == nullptr &&
                        D::TY && model->refine;
+    // (warm and past one wave per SIMD the fused two-wave kernel spills: Go2 65,536 warm 50.0 ->
+    // 44.5 M solves/s, so that case keeps the separate refinement pass)
+    const bool fused_warm = OSC_FUSE_REFINE_WARM && small && warm != nullptr && D::TY &&
+                            model->refine;
     if (warm == nullptr) {
       if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
@@ -3144,6 +3151,13 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
       else
         hipLaunchKernelGGL((osc_ipm_kernel<D, false, false>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+    } else if (fused_warm) {
+      // warm-started: the refinement runs in the same wavefront too, in pass 0 for the envs the
+      // warm start converged and in the cold fix-up pass for the ones it redoes
+      for (int pass = 0; pass < 2; ++pass) {
+        hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
+      }
     } else {
       for (int pass = 0; pass < 2; ++pass) {
         if (small)
@@ -3154,7 +3168,7 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
                              model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
       }
     }
-    if (D::TY && model->refine && !fused) {
+    if (D::TY && model->refine && !fused && !fused_warm) {
       if (small)
         hipLaunchKernelGGL((osc_refine_kernel<D, true>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x);

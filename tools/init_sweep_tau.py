@@ -33,6 +33,16 @@ def one(args):
         if "nofz0" in var:
             keep &= ~((h == 0) & (np.abs(G).sum(1) == 1) & (G.sum(1) == -1))
         p = (Hr, g, G[keep], h[keep])
+    if "jacobi" in var or "rownorm" in var:
+        Hr, g, G, h = p
+        d = np.ones(len(g))
+        if "jacobi" in var:
+            d = 1.0 / np.sqrt(np.abs(np.diag(Hr)))
+        Hr, g, G = d[:, None] * Hr * d[None, :], d * g, G * d[None, :]
+        if "rownorm" in var:
+            rn = 1.0 / np.linalg.norm(G, axis=1)
+            G, h = G * rn[:, None], h * rn
+        p = (Hr, g, G, h)
     return im.ipm(*p, eps_mu=EPS, max_iter=50, variant=var)[1]
 
 
