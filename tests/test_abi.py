@@ -47,6 +47,14 @@ def test_desc_from_yaml_matches_oracle(robot):
     ("walter_sr", "walter_sr/walter_sr_config.yaml"),
     ("walter_sr_wheels", "walter_sr_wheels/walter_sr_wheels_config.yaml"),
     ("walter_sr", "walter_sr/true_tumbling_mjjoint.yaml"),
+    # every WaLTER scenario config of the reference (same shape, different weights / targets)
+    ("walter_sr", "walter_sr/base_bad_stairs_climbing.yaml"),
+    ("walter_sr", "walter_sr/forward_velocity_front_tumbling.yaml"),
+    ("walter_sr", "walter_sr/forward_velocity_front_tumbling2.yaml"),
+    ("walter_sr", "walter_sr/slowtumbling.yaml"),
+    ("walter_sr", "walter_sr/slowtumbling_with_bodytargets_maybe_stairs.yaml"),
+    ("walter_sr", "walter_sr/stairclimbing_slightlybetter.yaml"),
+    ("walter_sr", "walter_sr/torso_tumbling_fail.yaml"),
 ])
 def test_reads_reference_yaml_files(robot, rel):
     """The native loader reads the reference's own config files (block lists, comments) and
@@ -57,6 +65,12 @@ def test_reads_reference_yaml_files(robot, rel):
     np.testing.assert_array_equal(np.array(d.w_pos[:m.ns]), m.w_pos)
     np.testing.assert_array_equal(np.array(d.w_rot[:m.ns]), m.w_rot)
     assert d.mu == m.mu
+    # a model the library has a kernel for (select_kernel, csrc/osc_batch.hip)
+    h = ctypes.c_void_p()
+    rc = _lib.lib().osc_model_create(ctypes.byref(d), ctypes.byref(h))
+    assert rc != 2, rel            # not OSC_ERR_UNSUPPORTED_DIMS (CPU-only: OSC_ERR_NO_DEVICE)
+    if rc == 0:
+        _lib.lib().osc_model_destroy(h)
 
 
 def test_error_codes():
