@@ -89,6 +89,9 @@ constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regio
 #ifndef OSC_SETUP_MFMA
 #define OSC_SETUP_MFMA 1
 #endif
+#ifndef OSC_HR_DIRECT
+#define OSC_HR_DIRECT 1
+#endif
 template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
@@ -152,7 +155,10 @@ struct Dims {
   static constexpr int JROWS = JG ? 3 * NC : S;                         // rows of A in LDS
   static constexpr int R1_A = JROWS * NAP + (JG ? 2 * even(S) : 0);    // A = [J | e | 0] (| e | w)
   static constexpr int O_E = JROWS * NAP, O_W = O_E + even(S);          // JG: e = b - t, row weights
-  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + (JG ? 0 : even(NY * NY));   // (T1 |) Hr
+  // [Hr | g] stored from phase D's MFMA registers (no LDS copy) -- JG models always, others with
+  // OSC_HR_DIRECT (A/B)
+  static constexpr bool HRD = JG || (MF && OSC_HR_DIRECT);
+  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + (HRD ? 0 : even(NY * NY));   // (T1 |) Hr
   static constexpr int R1 = cmax(R1_A, R1_D);
   static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
   static constexpr int O_A = 0;
@@ -931,7 +937,7 @@ __device__ __forceinline__ void setup_env(
             if (b < NY) {
               if (a == b && a < NU) v += wu2;
               if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
-              if constexpr (D::JG) {
+              if constexpr (D::HRD) {
                 wsv[D::W_HR + a * NY + b] = v;
                 wsv[D::W_HR + b * NY + a] = v;
               } else {
@@ -939,7 +945,7 @@ __device__ __forceinline__ void setup_env(
                 sHr[b * NY + a] = v;
               }
             } else {
-              if constexpr (D::JG) wsv[D::W_G + a] = v;
+              if constexpr (D::HRD) wsv[D::W_G + a] = v;
               else sG[a] = v;
             }
           }
@@ -1033,7 +1039,7 @@ __device__ __forceinline__ void setup_env(
   STAMP_BEGIN();
   // ---------------- write the reduced QP: workspace [Hr | g | U | X] -------------------------
   double* w = ws + static_cast<size_t>(env) * D::WS;
-  if constexpr (!D::JG) {   // (JG: written from phase D's registers)
+  if constexpr (!D::HRD) {   // (HRD: written from phase D's registers)
     for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
     for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
   }
