@@ -92,6 +92,9 @@ constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regio
 #ifndef OSC_HR_DIRECT
 #define OSC_HR_DIRECT 1
 #endif
+#ifndef OSC_WS_DIRECT   // X, H_dv, f_dv stored where they are formed (no copy-out phase)
+#define OSC_WS_DIRECT 1
+#endif
 template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
@@ -580,12 +583,22 @@ __device__ __forceinline__ void setup_env(
   // H_dv = 2 J'WJ + 2 w_reg I,  f_dv = 2 J'W (b - t)   (autogen.py:131-238, 304-319)
   // One 2x2 tile of the upper triangle per lane (column pairs read as one 16-byte LDS load);
   // each entry (i <= j) accumulates fma(w_r A_ri, A_rj) over r in order.
+  // (torque coordinates: H_dv and f_dv also go to the workspace from here, no write phase)
+  double* const wha = ws + static_cast<size_t>(env) * D::WS;
   auto put_ha = [&](int i, int j, double v) {
     if (i >= NA || j >= NA) return;
     v *= 2.0;
     if (i == j && i < NV) v += 2.0 * P->w_reg;
     sHa[i * NA + j] = v;
     sHa[j * NA + i] = v;
+    if constexpr (D::TY && OSC_WS_DIRECT) {
+      if (j < NV) {                          // H_dv (i <= j < NV), both triangles
+        wha[D::W_HD + i * NV + j] = v;
+        wha[D::W_HD + j * NV + i] = v;
+      } else if (j == NV && i < NV) {        // f_dv = the [J e] Gram's last column
+        wha[D::W_GD + i] = v;
+      }
+    }
   };
   if constexpr (kHaMfma<D>) {
     // FP64 MFMA (v_mfma_f64_16x16x4f64): 16x16 tiles of the upper block triangle, K = task rows
@@ -832,10 +845,19 @@ __device__ __forceinline__ void setup_env(
     });
     wave_sync();   // every lane has read X_b and U before any column is overwritten
     if (c < NY1P) {
+      double* const wx = ws + static_cast<size_t>(env) * D::WS + D::W_X;   // X: also to the workspace
 #pragma unroll
-      for (int r = 0; r < NB; ++r) sX[r * NY1P + c] = live ? xb[r] : 0.0;
+      for (int r = 0; r < NB; ++r) {
+        const double v = live ? xb[r] : 0.0;
+        sX[r * NY1P + c] = v;
+        if (OSC_WS_DIRECT) wx[r * NY1P + c] = v;
+      }
 #pragma unroll
-      for (int i = 0; i < NU; ++i) sX[(NB + i) * NY1P + c] = live ? xa[i] : 0.0;
+      for (int i = 0; i < NU; ++i) {
+        const double v = live ? xa[i] : 0.0;
+        sX[(NB + i) * NY1P + c] = v;
+        if (OSC_WS_DIRECT) wx[(NB + i) * NY1P + c] = v;
+      }
     }
     wave_sync();
     STAMP_END(8);
@@ -1044,8 +1066,10 @@ __device__ __forceinline__ void setup_env(
     for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
   }
   for (int i = lane; i < D::NUW * NY1P; i += kWave) w[D::W_U + i] = sU[i];
-  for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
-  if constexpr (D::TY) {
+  if (!D::TY || !OSC_WS_DIRECT) {   // (torque coordinates: X, H_dv, f_dv written where formed)
+    for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
+  }
+  if constexpr (D::TY && !OSC_WS_DIRECT) {
     for (int i = lane; i < NV * NV; i += kWave) w[D::W_HD + i] = sHa[(i / NV) * NA + i % NV];
     for (int i = lane; i < NV; i += kWave) w[D::W_GD + i] = sHa[i * NA + NV];
   }
