@@ -95,6 +95,9 @@ constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regio
 #ifndef OSC_WS_DIRECT   // X, H_dv, f_dv stored where they are formed (no copy-out phase)
 #define OSC_WS_DIRECT 1
 #endif
+#ifndef OSC_HD_DMA      // one-wave fused refinement: [H_dv | f_dv] by DMA behind K_A's LDL^T
+#define OSC_HD_DMA 1
+#endif
 template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
@@ -1912,8 +1915,9 @@ template <class D, bool SMALL, int RF>
 constexpr int refine_lds_extra() {
   if constexpr (RF == kRfNone || !D::TY) return 0;
   else if constexpr (RF == kRfFused && !SMALL) return 0;   // reads [X | H_dv | f_dv] from L2
-  else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())
-    return RefineLds<D>::SIZE - RefineLds<D>::HD;
+  else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())   // (DMA: whole 1 KB rows)
+    return OSC_HD_DMA ? (((RefineLds<D>::SIZE - RefineLds<D>::HD) / 2 + kWave - 1) / kWave) * kWave * 2
+                      : RefineLds<D>::SIZE - RefineLds<D>::HD;
   else return RefineLds<D>::SIZE;
 }
 template <class D, bool SMALL, int RF = kRfNone>
@@ -1991,7 +1995,7 @@ __device__ __forceinline__ void ipm_block(
     Batch2<LY::STAGE / 2, kRow> bs;
     bs.load(ws + static_cast<size_t>(env) * D::WS, l);
     const double mk = gmask[static_cast<size_t>(env) * NC + (l < NC ? l : 0)];
-    if constexpr (RF == kRfFused && !kRefG) {
+    if constexpr (RF == kRfFused && !kRefG && !(kXinHr && OSC_HD_DMA)) {
       // the refinement's own LDS block is free all along: its [X | H_dv | f_dv] (HRL:
       // [H_dv | f_dv]; X takes Hr's region later) is staged now, in the same memory latency
       // (by DMA instead, the allocator spills the one-wave Go2 kernel to scratch)
@@ -2760,6 +2764,28 @@ __device__ __forceinline__ void ipm_block(
                 (void)c;
 #endif
               });
+              if constexpr (OSC_HD_DMA) {
+                // [H_dv | f_dv] the same way, into the block's refinement region (not staged with
+                // the prologue's loads: 11 of the 27 MB every wave requests at once at 4,096 envs)
+                constexpr int NCH2 = (RefineLds<D>::SIZE - RefineLds<D>::HD) / 2;
+                constexpr int NT2 = (NCH2 + kWave - 1) / kWave;
+                static_assert(NT2 * kWave * 2 == refine_lds_extra<D, SMALL, RF>() &&
+                              D::W_HD == D::W_X + RefineLds<D>::HD && D::W_HD % 2 == 0,
+                              "[H_dv | f_dv] (whole DMA rows) in the refinement region");
+                const double2* src2 =
+                    reinterpret_cast<const double2*>(ws + static_cast<size_t>(eg) * D::WS + D::W_HD);
+                static_for<0, NT2>([&](auto T) {
+                  constexpr int t = decltype(T)::value;
+                  const int c = lane + kWave * t < NCH2 ? lane + kWave * t : NCH2 - 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+                  __builtin_amdgcn_global_load_lds(src2 + c, sm + g * kEnvLds + LY::IL + 2 * kWave * t,
+                                                   16, 0, 0);
+#else
+                  (void)src2;
+                  (void)c;
+#endif
+                });
+              }
             });
           }
         }
