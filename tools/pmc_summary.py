@@ -13,6 +13,7 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "prof")
 prefix = sys.argv[2] if len(sys.argv) > 2 else "r01_go2_4096"
+nenv = int(sys.argv[3]) if len(sys.argv) > 3 else 4096   # Go2 envs per launch of the profiled run
 dst = os.path.join(REPO, "profiles")
 
 
@@ -65,11 +66,13 @@ for k, cs in counters.items():
 json.dump(out, open(os.path.join(dst, f"{prefix}_counters.json"), "w"), indent=1)
 hb = [v.get("hbm_bytes") for v in out["kernels"].values()]
 if hb and all(h is not None for h in hb):
-    json.dump({"robot": "unitree_go2", "nenv": 4096, "bytes_per_launch": sum(hb),
+    # pmc_traffic.json is what bench.py's default (4,096-env) line reads; other sizes beside it
+    tname = "pmc_traffic.json" if nenv == 4096 else f"pmc_traffic_{nenv}.json"
+    json.dump({"robot": "unitree_go2", "nenv": nenv, "bytes_per_launch": sum(hb),
                "per_kernel": {k: v.get("hbm_bytes") for k, v in out["kernels"].items()},
                "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per kernel (gfx950 "
                              "FETCH_SIZE halving for 16 B/lane reads; 8 B/lane reads uncalibrated)",
-               "algorithmic_bytes_per_launch": 7664 * 4096,
+               "algorithmic_bytes_per_launch": 7664 * nenv,
                "source": [f"profiles/{prefix}_pmc_fetch.csv", f"profiles/{prefix}_pmc_write.csv"]},
-              open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+              open(os.path.join(dst, tname), "w"), indent=1)
 print(json.dumps(out, indent=1))
