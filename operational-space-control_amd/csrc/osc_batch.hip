@@ -1920,10 +1920,16 @@ constexpr int refine_lds_extra() {
                       : RefineLds<D>::SIZE - RefineLds<D>::HD;
   else return RefineLds<D>::SIZE;
 }
+// Two-wave variant: minimum LDS request in doubles (0 = its own need).  A larger request caps
+// the wavefronts resident per CU, and with them the Hr working set each XCD's L2 must hold
+#ifndef OSC_LARGE_LDS_MIN
+#define OSC_LARGE_LDS_MIN 0
+#endif
 template <class D, bool SMALL, int RF = kRfNone>
 constexpr int ipm_lds_doubles() {
   constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>();
-  return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
+  return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2)
+               : cmax(kEnvPerWave * il, OSC_LARGE_LDS_MIN);
 }
 
 // The body of one IPM wavefront (envs 4 blk .. 4 blk + 3); `sm` is its ipm_lds_doubles<D, SMALL>
