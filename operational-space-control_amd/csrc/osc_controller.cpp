@@ -9,6 +9,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <utility>
@@ -128,8 +129,7 @@ Status OperationalSpaceController::initialize_optimization() {
   hipStream_t stream = nullptr;
   if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&d_in_), in_doubles * sizeof(double)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&d_out_), (even(nu_) + even(n_)) * sizeof(double)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&d_info_), 2 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_out_), (even(nu_) + even(n_) + 1) * sizeof(double)) != hipSuccess ||
       hipMalloc(&d_ws_, ws_bytes_) != hipSuccess ||
       osc_warm_state_bytes(model_, 1, &warm_bytes_) != OSC_OK ||
       hipMalloc(reinterpret_cast<void**>(&d_warm_), warm_bytes_) != hipSuccess ||
@@ -139,7 +139,18 @@ Status OperationalSpaceController::initialize_optimization() {
     return InternalError("device allocation failed");
   }
   stream_ = stream;
-  h_in_.assign(in_doubles, 0.0);
+  // tau | x | (status, iters) in one device block, so the tick's results come back in one copy
+  out_doubles_ = even(nu_) + even(n_);
+  d_info_ = reinterpret_cast<int32_t*>(d_out_ + out_doubles_);
+  if (hipHostMalloc(reinterpret_cast<void**>(&h_in_), in_doubles * sizeof(double),
+                    hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&h_out_), (out_doubles_ + 1) * sizeof(double),
+                    hipHostMallocDefault) != hipSuccess) {
+    release_device();
+    return InternalError("pinned host allocation failed");
+  }
+  std::memset(h_in_, 0, in_doubles * sizeof(double));
+  if (const char* e = std::getenv("OSC_TICK_GRAPH")) use_graph_ = std::atoi(e) != 0;
   optimization_initialized_ = true;
   return Status::Ok();
 }
@@ -219,7 +230,7 @@ Status OperationalSpaceController::tick_gpu_kinematics_locked() {
       state_.motor_velocity.size() != static_cast<size_t>(nu_) || state_.body_rotation.size() != 4 ||
       state_.linear_body_velocity.size() != 3 || state_.angular_body_velocity.size() != 3)
     return InvalidArgumentError("State / targets size mismatch");
-  double* h = h_in_.data();
+  double* h = h_in_;
   double* qpos = h;
   double* qvel = h + even(nq_);
   double* T = qvel + even(nv_);
@@ -233,14 +244,88 @@ Status OperationalSpaceController::tick_gpu_kinematics_locked() {
   std::memcpy(T, targets_.data(), targets_.size() * sizeof(double));
   std::memcpy(mask, state_.contact_mask.data(), nc_ * sizeof(double));
   const size_t off = static_cast<size_t>(mask - h) + even(nc_);
+  return launch_tick_locked(1, off * sizeof(double));
+}
+
+// One tick's stream work: H2D of the staged inputs, the batched entry point with nenv = 1
+// (warm-started from the previous tick, as the reference's SetWarmStart :519-526), D2H of
+// tau | x | status | iters into pinned memory.  Every pointer is fixed at initialization, so
+// the sequence is the same every tick.
+Status OperationalSpaceController::enqueue_tick_locked(int kind, size_t in_bytes) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  if (hipMemcpyAsync(d_in_, h, off * sizeof(double), hipMemcpyHostToDevice, stream) != hipSuccess)
+  if (hipMemcpyAsync(d_in_, h_in_, in_bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
     return InternalError("host to device copy failed");
-  return from_osc(osc_batch_solve_qpos_warm(model_, kin_, 1, d_in_, d_in_ + (qvel - h),
-                                            d_in_ + (T - h), d_in_ + (mask - h), d_out_,
-                                            d_out_ + even(nu_), d_info_, d_info_ + 1, d_warm_,
-                                            warm_bytes_, d_ws_, ws_bytes_, stream_),
+  Status st;
+  if (kind == 1) {
+    const size_t q = even(nq_), v = q + even(nv_), t = v + even(ns_ * 6);
+    st = from_osc(osc_batch_solve_qpos_warm(model_, kin_, 1, d_in_, d_in_ + q, d_in_ + v,
+                                            d_in_ + t, d_out_, d_out_ + even(nu_), d_info_,
+                                            d_info_ + 1, d_warm_, warm_bytes_, d_ws_, ws_bytes_,
+                                            stream_),
                   "osc_batch_solve_qpos_warm");
+  } else {
+    const size_t nv = nv_, s = 6 * static_cast<size_t>(ns_);
+    const size_t sizes[6] = {nv * nv, nv, s * nv, s, static_cast<size_t>(ns_) * 6,
+                             static_cast<size_t>(nc_)};
+    double* dptr[6];
+    size_t off = 0;
+    for (int k = 0; k < 6; ++k) {
+      dptr[k] = d_in_ + off;
+      off += even(sizes[k]);
+    }
+    st = from_osc(osc_batch_solve_warm(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4],
+                                       dptr[5], d_out_, d_out_ + even(nu_), d_info_, d_info_ + 1,
+                                       d_warm_, warm_bytes_, d_ws_, ws_bytes_, stream_),
+                  "osc_batch_solve_warm");
+  }
+  if (!st.ok()) return st;
+  if (hipMemcpyAsync(h_out_, d_out_, (out_doubles_ + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                     stream) != hipSuccess)
+    return InternalError("device to host copy failed");
+  return Status::Ok();
+}
+
+// The tick as one hipGraph (OSC_TICK_GRAPH=1): captured on the first tick of a kind and replayed
+// afterwards (one submission instead of two copies, three or four kernel launches and two
+// copies).  A capture the runtime refuses falls back to launching the same work directly.  Off by
+// default: on MI355X / ROCm 7 the replay is slower than the direct launches from pinned staging
+// (Go2 tick median 98 vs 92 us, WaLTER 109 vs 103 us; profiles/r02_tick_graph_ab.txt).
+Status OperationalSpaceController::launch_tick_locked(int kind, size_t in_bytes) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (graph_exec_ && graph_kind_ == kind && graph_in_bytes_ == in_bytes) {
+    if (hipGraphLaunch(static_cast<hipGraphExec_t>(graph_exec_), stream) != hipSuccess)
+      return InternalError("tick graph launch failed");
+    return Status::Ok();
+  }
+  drop_graph();
+  if (use_graph_ && hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed) == hipSuccess) {
+    Status st = enqueue_tick_locked(kind, in_bytes);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(stream, &g);
+    hipGraphExec_t exec = nullptr;
+    if (st.ok() && ec == hipSuccess && g &&
+        hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) == hipSuccess) {
+      (void)hipGraphDestroy(g);
+      graph_exec_ = exec;
+      graph_kind_ = kind;
+      graph_in_bytes_ = in_bytes;
+      if (hipGraphLaunch(exec, stream) != hipSuccess)
+        return InternalError("tick graph launch failed");
+      return Status::Ok();
+    }
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (!st.ok()) return st;   // argument errors are reported as the direct path reports them
+    use_graph_ = false;        // capture unsupported here: direct launches from now on
+  }
+  return enqueue_tick_locked(kind, in_bytes);
+}
+
+void OperationalSpaceController::drop_graph() {
+  if (graph_exec_) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(graph_exec_));
+  graph_exec_ = nullptr;
+  graph_kind_ = -1;
+  graph_in_bytes_ = 0;
 }
 
 // The body of the reference's control_loop (:556-574), caller holds the mutex.
@@ -260,45 +345,31 @@ Status OperationalSpaceController::tick_locked() {
       state_.contact_mask.size() != static_cast<size_t>(nc_))
     return InvalidArgumentError("OSCData / targets / contact_mask size mismatch");
   // pack M | C | J | b | T | mask (row-major per block, each block padded to 16 B)
-  double* h = h_in_.data();
+  double* h = h_in_;
   const double* blocks[6] = {osc_data_.mass_matrix.data(), osc_data_.coriolis_matrix.data(),
                              osc_data_.taskspace_jacobian.data(), osc_data_.taskspace_bias.data(),
                              targets_.data(), state_.contact_mask.data()};
   const size_t sizes[6] = {nv * nv, nv, s * nv, s, static_cast<size_t>(ns_) * 6,
                            static_cast<size_t>(nc_)};
-  double* dptr[6];
   size_t off = 0;
   for (int k = 0; k < 6; ++k) {
     std::memcpy(h + off, blocks[k], sizes[k] * sizeof(double));
-    dptr[k] = d_in_ + off;
     off += even(sizes[k]);
   }
-  hipStream_t stream = static_cast<hipStream_t>(stream_);
-  if (hipMemcpyAsync(d_in_, h, off * sizeof(double), hipMemcpyHostToDevice, stream) != hipSuccess)
-    return InternalError("host to device copy failed");
-  double* d_tau = d_out_;
-  double* d_x = d_out_ + even(nu_);
-  // warm-started from the previous tick, as the reference's SetWarmStart (:519-526)
-  st = from_osc(osc_batch_solve_warm(model_, 1, dptr[0], dptr[1], dptr[2], dptr[3], dptr[4],
-                                     dptr[5], d_tau, d_x, d_info_, d_info_ + 1, d_warm_,
-                                     warm_bytes_, d_ws_, ws_bytes_, stream_),
-                "osc_batch_solve_warm");
+  st = launch_tick_locked(0, off * sizeof(double));
   if (!st.ok()) return st;
   return fetch_outputs_locked();
 }
 
 // Copy tau | x | status | iters back and publish them (torque_command = x[nv : nv+nu], :573).
 Status OperationalSpaceController::fetch_outputs_locked() {
-  hipStream_t stream = static_cast<hipStream_t>(stream_);
-  std::vector<double> out(even(nu_) + n_);
-  int32_t info[2] = {0, 0};
-  if (hipMemcpyAsync(out.data(), d_out_, out.size() * sizeof(double), hipMemcpyDeviceToHost,
-                     stream) != hipSuccess ||
-      hipMemcpyAsync(info, d_info_, sizeof(info), hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipStreamSynchronize(stream) != hipSuccess)
+  // (the tick's D2H copies into h_out_ were enqueued with it)
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream_)) != hipSuccess)
     return InternalError("device to host copy failed");
-  torque_.assign(out.begin(), out.begin() + nu_);            // = solution[nv : nv+nu] (:573)
-  solution_.assign(out.begin() + even(nu_), out.begin() + even(nu_) + n_);
+  int32_t info[2];
+  std::memcpy(info, h_out_ + out_doubles_, sizeof(info));
+  torque_.assign(h_out_, h_out_ + nu_);                      // = solution[nv : nv+nu] (:573)
+  solution_.assign(h_out_ + even(nu_), h_out_ + even(nu_) + n_);
   status_ = info[0];
   iters_ = info[1];
   return Status::Ok();
@@ -328,9 +399,12 @@ void OperationalSpaceController::control_loop() {
 
 void OperationalSpaceController::release_device() {
   if (stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+  drop_graph();
+  if (h_in_) (void)hipHostFree(h_in_);
+  if (h_out_) (void)hipHostFree(h_out_);
+  h_in_ = h_out_ = nullptr;
   if (d_in_) (void)hipFree(d_in_);
   if (d_out_) (void)hipFree(d_out_);
-  if (d_info_) (void)hipFree(d_info_);
   if (d_ws_) (void)hipFree(d_ws_);
   if (d_warm_) (void)hipFree(d_warm_);
   d_warm_ = nullptr;
