@@ -35,8 +35,11 @@ def driver():
     return EXE
 
 
-def run(*args):
-    r = subprocess.run([driver(), *args], capture_output=True, text=True, timeout=120)
+def run(*args, graph=None):
+    env = dict(os.environ)
+    if graph is not None:    # OSC_TICK_GRAPH=1: the tick replayed as one captured hipGraph
+        env["OSC_TICK_GRAPH"] = graph
+    r = subprocess.run([driver(), *args], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
 
@@ -62,14 +65,15 @@ def test_lifecycle_preconditions(robot):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["0", "1"])
 @pytest.mark.parametrize("case", ["go2_standing", "go2_tumbling_mask", "walter_standing"])
-def test_controller_tick_and_thread_match_oracle(gpu, case, tmp_path):
+def test_controller_tick_and_thread_match_oracle(gpu, case, graph, tmp_path):
     g = np.load(os.path.join(GOLDEN, case + ".npz"))
     robot = str(g["robot"])
     fx = tmp_path / "fixture.bin"
     parts = [g[k][0].astype(np.float64).ravel() for k in ("M", "C", "J", "b", "T", "mask", "tau")]
     np.concatenate(parts).tofile(fx)
-    out = run("solve", robot, str(fx))
+    out = run("solve", robot, str(fx), graph=graph)
     assert out["status"] == 0 and out["iters"] > 0
     assert out["err_step"] <= 1e-5 and out["err_thread"] <= 1e-5, out   # tests/test_gpu_parity.py
     assert out["slice"] == 0.0                            # torque = solution[nv:nv+nu] (osc.h:573)
@@ -91,8 +95,9 @@ def test_gpu_kinematics_controller_arguments(robot):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["0", "1"])
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])
-def test_gpu_kinematics_controller_matches_oracle(gpu, robot, tmp_path):
+def test_gpu_kinematics_controller_matches_oracle(gpu, robot, graph, tmp_path):
     """The controller without a KinematicsFn: State -> qpos/qvel (update_mj_data) -> GPU
     kinematics -> QP -> torque, against the oracle chain (kinematics oracle -> reference QP ->
     exact optimum)."""
@@ -112,7 +117,7 @@ def test_gpu_kinematics_controller_matches_oracle(gpu, robot, tmp_path):
     tau = torque(model, solve_exact(model, build_qp(model, M, C, J, b, T, mask), M, C, J).x)
     fx = tmp_path / "fixture.bin"
     np.concatenate([qpos[0], qvel[0], T.ravel(), mask, tau]).astype(np.float64).tofile(fx)
-    out = run("qpos", robot, str(fx))
+    out = run("qpos", robot, str(fx), graph=graph)
     assert out["status"] == 0
     assert out["err_step"] <= 1e-5 and out["err_thread"] <= 1e-5, out
     assert out["thread"] == OK and out["stop"] == OK and out["clean"] == OK
