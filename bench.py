@@ -584,11 +584,19 @@ def main(argv=None) -> None:
 
     ri = rank_info()
     world, rank, local = ri.world, ri.rank, ri.local
+    # OSC_DIST_BACKEND=gloo: rehearsal of the N-rank path on a box with fewer GPUs than ranks
+    # (ranks share the devices round-robin; barriers and the reduction over gloo on the host)
+    backend = os.environ.get("OSC_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)   # RCCL; barriers + timing reduction only
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)   # RCCL; barriers + timing reduction only
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         dist_barrier(world)
@@ -619,6 +627,9 @@ def main(argv=None) -> None:
             line["single_env"] = single_env(args.robot, args.single_env_ticks)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.robot, args.cpu_seconds, args.cpu_cores)
+        if backend != "nccl" and world > 1:   # not a multi-GPU measurement
+            line["rehearsal"] = (f"{backend}: {world} ranks on {torch.cuda.device_count()} "
+                                 f"GPU(s), ranks sharing devices")
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

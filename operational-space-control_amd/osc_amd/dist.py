@@ -49,6 +49,8 @@ def reduce_stats(world: int, device: torch.device, nenv: int, elapsed_s: float, 
                  ipm_ms: float, n_converged: int) -> JobStats:
     """Max-over-ranks timing and summed convergence counts (one all_reduce each)."""
     if world > 1:
+        if torch.distributed.get_backend() == "gloo":   # CPU tests / one-GPU rehearsal
+            device = torch.device("cpu")
         t = torch.tensor([elapsed_s, setup_ms + ipm_ms, setup_ms, ipm_ms], device=device,
                          dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
