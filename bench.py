@@ -284,7 +284,11 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
                                 if args.mixed_mode == "multi" else
                                 f"osc_setup_kernel + osc_ipm_kernel x 2 models ({args.mixed_mode})"),
                      "kernel_ms": stats.kernel_ms},
-        "converged_frac": stats.converged}), flush=True)
+        "converged_frac": stats.converged,
+        **({"rehearsal": f"{os.environ['OSC_DIST_BACKEND']}: {world} ranks on "
+                         f"{torch.cuda.device_count()} GPU(s), ranks sharing devices"}
+           if world > 1 and os.environ.get("OSC_DIST_BACKEND", "nccl") != "nccl" else {})}),
+          flush=True)
 
 
 def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
