@@ -1925,9 +1925,20 @@ constexpr int refine_lds_extra() {
 #ifndef OSC_LARGE_LDS_MIN
 #define OSC_LARGE_LDS_MIN 0
 #endif
+// Two-wave variant: Hr's upper triangle packed in LDS (row i at i NY - i (i - 1) / 2; 300 doubles
+// per Go2 env, 9.6 KB per wavefront beside its 7.9 KB: still two waves per SIMD) instead of each
+// lane re-reading its two Hr columns from the workspace every iteration
+#ifndef OSC_HR_PACKED
+#define OSC_HR_PACKED 0
+#endif
+template <class D, bool SMALL, int RF>
+constexpr int hr_packed_lds() {   // doubles per env
+  return (OSC_HR_PACKED && !SMALL && RF != kRfOnly) ? even(D::NY * (D::NY + 1) / 2) : 0;
+}
 template <class D, bool SMALL, int RF = kRfNone>
 constexpr int ipm_lds_doubles() {
-  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>();
+  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>() +
+                     hr_packed_lds<D, SMALL, RF>();
   return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2)
                : cmax(kEnvPerWave * il, OSC_LARGE_LDS_MIN);
 }
@@ -1963,8 +1974,10 @@ __device__ __forceinline__ void ipm_block(
     write_out = valid && (!fixup || redo);
   }
 
-  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>();
+  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>() + hr_packed_lds<D, SMALL, RF>();
   double* B = sm + grp * kEnvLds;
+  constexpr bool kHrPk = hr_packed_lds<D, SMALL, RF>() > 0;
+  double* sHp = B + LY::IL + refine_lds_extra<D, SMALL, RF>();   // packed Hr (kHrPk)
   // refinement: [X | H_dv | f_dv] of this env; a fused pass with Hr in LDS keeps X in Hr's region
   constexpr bool kXinHr = RF == kRfFused && HRL;
   double* sRX = kXinHr ? B + LY::I_HR : B + LY::IL + RefineLds<D>::X;
@@ -2014,6 +2027,24 @@ __device__ __forceinline__ void ipm_block(
     }
     bs.store(B, l);
     if (l < NC) sMask[l] = mk;
+  }
+  if constexpr (kHrPk) {
+    // row i of Hr's upper triangle: lane l copies entries j = i + l and i + l + 16
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      constexpr int kS = 2;
+      double v[kS];
+#pragma unroll
+      for (int t = 0; t < kS; ++t) {
+        const int j = i + l + kRow * t;
+        v[t] = wsw[lane_off + static_cast<unsigned>(i * NY + (j < NY ? j : NY - 1))];
+      }
+#pragma unroll
+      for (int t = 0; t < kS; ++t) {
+        const int j = i + l + kRow * t;
+        if (j < NY) sHp[i * NY - i * (i - 1) / 2 + (j - i)] = v[t];
+      }
+    }
   }
   const double* sHr = B + LY::I_HR;
   wave_sync();
@@ -2261,6 +2292,16 @@ __device__ __forceinline__ void ipm_block(
       for (int i = 0; i < NY; ++i) {
         c0[i] = hr0[i];
         c1[i] = hr1[i];
+      }
+    } else if constexpr (kHrPk) {
+      // Hr[i][j] = packed (min, max): row i's entry j at i NY - i (i - 1) / 2 + j - i
+      const int p0 = j0 * NY - j0 * (j0 - 1) / 2 - j0;
+      const int p1 = jj1 * NY - jj1 * (jj1 - 1) / 2 - jj1;
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        const int oi = i * NY - i * (i - 1) / 2 - i;
+        c0[i] = sHp[i <= j0 ? oi + j0 : p0 + i];
+        c1[i] = sHp[i <= jj1 ? oi + jj1 : p1 + i];
       }
     } else {
       unsigned off = lane_off;
