@@ -2294,14 +2294,18 @@ __device__ __forceinline__ void ipm_block(
         c1[i] = hr1[i];
       }
     } else if constexpr (kHrPk) {
-      // Hr[i][j] = packed (min, max): row i's entry j at i NY - i (i - 1) / 2 + j - i
-      const int p0 = j0 * NY - j0 * (j0 - 1) / 2 - j0;
-      const int p1 = jj1 * NY - jj1 * (jj1 - 1) / 2 - jj1;
+      // Hr[i][j] = packed (min, max): row i's entry j at i NY - i (i - 1) / 2 + j - i.  The
+      // lane's bases are formed here, every time (hidden from loop-invariant hoisting, as the
+      // workspace path's: kept live across the loop they spill)
+      int a0 = j0, a1 = jj1;
+      asm volatile("" : "+v"(a0), "+v"(a1));
+      const double* q0 = sHp + (a0 * NY - a0 * (a0 - 1) / 2 - a0);
+      const double* q1 = sHp + (a1 * NY - a1 * (a1 - 1) / 2 - a1);
 #pragma unroll
       for (int i = 0; i < NY; ++i) {
         const int oi = i * NY - i * (i - 1) / 2 - i;
-        c0[i] = sHp[i <= j0 ? oi + j0 : p0 + i];
-        c1[i] = sHp[i <= jj1 ? oi + jj1 : p1 + i];
+        c0[i] = (i <= a0) ? sHp[oi + a0] : q0[i];
+        c1[i] = (i <= a1) ? sHp[oi + a1] : q1[i];
       }
     } else {
       unsigned off = lane_off;
