@@ -13,20 +13,20 @@
 //          (+-fx +-fy - mu fz) <= 0 per contact, fz in [z_lb, z_ub] * mask, u in [u_lb, u_ub]
 //
 // Method:
-//   1. u is eliminated exactly from the actuated dynamics rows, and the base accelerations
-//      dv_b from the unactuated rows through the base block M_bb only:
-//         dv_b = M_bb^-1 (-M_ba dv_a + Jc_b z - C_b),   u = M_a dv + C_a - Jc_a z.
-//      The unknowns y = (dv_a, z) (24 Go2 / 32 WaLTER) carry a dense reduced Hessian Hr and
-//      gradient g.  Inverting only M_bb keeps the regularisation-only curvature
-//      (2 w_reg = 2e-4: internal contact forces) resolvable in fp64.
+//   1. The dynamics rows are eliminated exactly in torque coordinates y = (u, z) (24 Go2 /
+//      32 WaLTER unknowns): dv = X [y; 1] = M^-1 (B u + Jc z - C) by block elimination on the
+//      base block M_bb and the Schur complement of the actuated block, so the torque bounds are
+//      plain bounds on y.  y carries a dense reduced Hessian Hr = X'H_dv X + diag and gradient g.
 //   2. Mehrotra predictor-corrector interior point on  min 1/2 y'Hr y + g'y  s.t. G y <= h,
-//      G = [+-U (torque bounds, dense rows); pyramid + fz bound rows (sparse)].  Newton matrix
+//      G = [+-e_q (torque bounds); pyramid + fz bound rows (sparse)].  Newton matrix
 //      K = Hr + G' diag(lambda/s) G, LDL^T with "Cholesky-infinity" pivots.
+//   3. A full-space refinement on the converged active set removes the error of the explicitly
+//      formed fp64 Hr (its residual never goes through Hr).
 //
-// Two kernels, one workspace (per env [g | U | Hr | X], fp64; no U in torque coordinates):
+// Two kernels, one workspace (per env [g | Hr | X | H_dv | f_dv], fp64):
 //   osc_setup_kernel  one 64-lane wavefront per environment.  Inputs are staged HBM -> LDS
-//                     with 16-byte loads; the dense products (J'WJ, the reduced Hessian) give
-//                     every lane several output entries.
+//                     with 16-byte loads; the dense products (J'WJ, the reduced Hessian) run on
+//                     the FP64 matrix cores or as 2x2 VALU tiles.
 //   osc_ipm_kernel    FOUR environments per wavefront, one 16-lane DPP row each.  The Newton
 //                     matrix lives in registers, lane l holding columns l and l+16.  The
 //                     right-looking LDL^T broadcasts the pivot column inside each row with
@@ -77,37 +77,22 @@ struct DevParams {
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regions 16-B aligned
 
-// TY_ selects the reduced coordinates: false -> y = (dv_a, z), u = U [y; 1] (dense torque rows,
-// only the base block M_bb is inverted); true -> y = (u, z), dv = X [y; 1] = M^-1 (B u + Jc z - C)
-// over all nv rows, so the torque bounds are plain bounds on y (diagonal in the Newton matrix).
-// Assembly products on the FP64 matrix cores (torque-coordinate models): bit 0 = T1 and Hr
-// (phase D), bit 1 = Ha (phase B) for every model (by default only where NA <= 16); 0 = VALU
-// 2x2 tiles everywhere.  FP64 MFMA has the FP64 VALU's
-// peak on gfx950 (tools/mb_mfma64.hip: ~70 clocks per 16x16x4), so it only pays where it saves
-// LDS round trips: phase D keeps T1 in registers; Ha's padded 16x16 tiles (19 -> 32) cost more
-// than the VALU's exact 2x2 tiles (Go2 4,096: phase B 7.7k vs 3.5k clocks per wave)
-#ifndef OSC_SETUP_MFMA
-#define OSC_SETUP_MFMA 1
-#endif
-#ifndef OSC_HR_DIRECT
-#define OSC_HR_DIRECT 1
-#endif
-#ifndef OSC_WS_DIRECT   // X, H_dv, f_dv stored where they are formed (no copy-out phase)
-#define OSC_WS_DIRECT 1
-#endif
-#ifndef OSC_HD_DMA      // one-wave fused refinement: [H_dv | f_dv] by DMA behind K_A's LDL^T
-#define OSC_HD_DMA 1
-#endif
-template <int NV_, int NU_, int NC_, int NS_, bool TY_ = false>
+// Reduced coordinates y = (u, z): dv = X [y; 1] = M^-1 (B u + Jc z - C) over all nv rows, so the
+// torque bounds are plain bounds on y (diagonal in the Newton matrix).  The dense assembly
+// products run on the FP64 matrix cores where that saves LDS round trips (FP64 MFMA has the FP64
+// VALU's peak on gfx950, tools/mb_mfma64.hip: ~70 clocks per 16x16x4): T1 = H_dv X and
+// [Hr | g] = X'T1 always (T1 stays in registers), Ha = 2 [J e]'W[J e] where [J e] fits one
+// 16-column tile (WaLTER, NA = 15); Go2's 19 columns would pad to 32 and stay on exact 2x2 VALU
+// tiles (Go2 4,096: phase B 7.7k vs 3.5k clocks per wave).  X, H_dv, f_dv and [Hr | g] are stored
+// to the workspace where they are formed (no copy-out phase).
+template <int NV_, int NU_, int NC_, int NS_>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
-  static constexpr bool TY = TY_;
   static constexpr int NB = NV - NU;          // unactuated (floating-base) dofs
-  static constexpr int NXR = TY ? NV : NB;    // rows of X: the dv entries that are not in y
   static constexpr int NZ = 3 * NC;
-  static constexpr int NY = NU + NZ;          // reduced variables (dv_a or u, z)
+  static constexpr int NY = NU + NZ;          // reduced variables (u, z)
   static constexpr int NY1 = NY + 1;          // + affine column
-  static constexpr int NY1P = even(NY1);      // padded row stride of U and X
+  static constexpr int NY1P = even(NY1);      // padded row stride of X
   static constexpr int S = 6 * NS;            // task rows
   static constexpr int MI = 2 * NU + 6 * NC;  // inequality rows (u box, pyramid, fz box)
   static constexpr int NX = NV + NU + NZ;     // design vector
@@ -120,67 +105,49 @@ struct Dims {
   static_assert(NU <= kRow && NB <= kRow, "IPM: one torque / base row per lane");
   static_assert(NB >= 1 && NB <= 8, "floating-base block");
 
-  // ---- workspace per env (doubles): [g | U | Hr | X] ----
+  // ---- workspace per env (doubles): [g | Hr | X | H_dv | f_dv | W_SOL] ----
   static constexpr int W_G = 0;
-  static constexpr int NUW = TY ? 0 : NU;     // rows of U kept (TY: U = [I | 0] is implicit)
-  static constexpr int W_U = even(NY);
-  static constexpr int W_HR = W_U + NUW * NY1P;
+  static constexpr int W_HR = even(NY);
   static constexpr int W_X = W_HR + even(NY * NY);
-  // torque coordinates: H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t), for the full-space
-  // refinement after the interior point (its gradient never goes through Hr)
-  static constexpr int W_HD = W_X + NXR * NY1P;
-  static constexpr int W_GD = W_HD + (TY ? NV * NV : 0);
+  // H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t), for the full-space refinement after the
+  // interior point (its gradient never goes through Hr)
+  static constexpr int W_HD = W_X + NV * NY1P;
+  static constexpr int W_GD = W_HD + NV * NV;
   // interior-point result handed to the refinement kernel: [y | q (lambda on rows with
   // lambda > s, else 0; row slots) | status]
-  static constexpr int W_SOL = W_GD + (TY ? even(NV) : 0);
-  static constexpr int W_SQ = W_SOL + even(NY);
-  static constexpr int W_SST = W_SQ + NRL * 16;
-  static constexpr int WS = W_SOL + (TY ? even(NY) + NRL * 16 + 2 : 0);
+  static constexpr int W_SOL = W_GD + even(NV);
+  static constexpr int WS = W_SOL + even(NY) + NRL * 16 + 2;
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
   static constexpr int WW_Y = 2;
   static constexpr int WW_L = WW_Y + even(NY);
   static constexpr int WW_M = WW_L + NRL * 16;     // contact mask the state was solved with
   static constexpr int WW = WW_M + even(NC);
 
-  // ---- setup-kernel LDS (doubles).  R1/R2 are reused between phases.  Every matrix that the
-  // 2x2-tiled products read by column pairs (A = [J | e | 0], X, U, T1) has an even row stride,
-  // so a column pair is one 16-byte LDS read. ----
+  // ---- setup-kernel LDS (doubles).  Every matrix that the 2x2-tiled products read by column
+  // pairs (A = [J | e | 0]) has an even row stride, so a column pair is one 16-byte LDS read. ----
   static constexpr int NAP = even(NA);                   // [J | e (| 0)] row stride
-  static constexpr int NA2 = NAP / 2, NY2 = NY1P / 2;    // column pairs
+  static constexpr int NA2 = NAP / 2;                    // column pairs
   static constexpr int NBA = NA2 * (NA2 + 1) / 2;        // Ha tiles (upper triangle)
-  static constexpr int NBT = (NV / 2) * NY2;             // T1 tiles
-  static constexpr int NBH = NY2 * (NY2 + 1) / 2;        // Hr | g tiles (upper triangle)
-  static constexpr bool MF = (OSC_SETUP_MFMA & 1) && TY;   // MFMA products: T1 stays in registers
-  // Ha on MFMA (forced by bit 1, else where [J e] fits one 16-column tile: WaLTER, NA = 15)
-  static constexpr bool HAM = TY && ((OSC_SETUP_MFMA & 2) || ((OSC_SETUP_MFMA & 1) && NA <= 16));
-  // J not staged: Ha's MFMA fragments come straight from global memory, LDS holds only the
-  // contact rows phase C reads (WaLTER: 102 x 16 -> 24 x 16 doubles), and [Hr | g] go to the
-  // workspace from phase D's registers (no LDS copy): setup LDS 20.4 -> 10.4 KB.  (Go2 keeps the
-  // LDS copy of Hr: the register-direct stores took its VGPRs from 108 to the 252 cap.)
-  static constexpr bool JG = HAM && MF;
+  // Ha on MFMA where [J e] fits one 16-column tile (WaLTER, NA = 15).  J is then not staged:
+  // Ha's MFMA fragments come straight from global memory and LDS holds only the contact rows
+  // phase C reads (WaLTER: 102 x 16 -> 24 x 16 doubles): setup LDS 20.4 -> 10.4 KB.
+  static constexpr bool JG = NA <= 16;
   static constexpr int JROWS = JG ? 3 * NC : S;                         // rows of A in LDS
-  static constexpr int R1_A = JROWS * NAP + (JG ? 2 * even(S) : 0);    // A = [J | e | 0] (| e | w)
+  static constexpr int R1 = JROWS * NAP + (JG ? 2 * even(S) : 0);      // A = [J | e | 0] (| e | w)
   static constexpr int O_E = JROWS * NAP, O_W = O_E + even(S);          // JG: e = b - t, row weights
-  // [Hr | g] stored from phase D's MFMA registers (no LDS copy) -- JG models always, others with
-  // OSC_HR_DIRECT (A/B)
-  static constexpr bool HRD = JG || (MF && OSC_HR_DIRECT);
-  static constexpr int R1_D = (MF ? 0 : NV * NY1P) + (HRD ? 0 : even(NY * NY));   // (T1 |) Hr
-  static constexpr int R1 = cmax(R1_A, R1_D);
-  static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C, later g
+  static constexpr int R2 = even(NV * NV) + even(NV);                   // M | C
   static constexpr int O_A = 0;
-  static constexpr int O_T1 = 0, O_HR = MF ? 0 : NV * NY1P;
-  static constexpr int O_M = R1, O_C = R1 + even(NV * NV), O_G = R1;
+  static constexpr int O_M = R1, O_C = R1 + even(NV * NV);
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
-  static constexpr int O_U = O_X + NXR * NY1P;
-  static constexpr int O_MASK = O_U + NUW * NY1P;
+  static constexpr int O_MASK = O_X + NV * NY1P;
   static constexpr int SMEM = O_MASK + even(NC);
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
 };
 
-// ---- IPM-kernel LDS per env (doubles): workspace prefix [g | U (| Hr)] + vectors.
+// ---- IPM-kernel LDS per env (doubles): workspace prefix [g (| Hr)] + vectors.
 // Large batches (two waves per SIMD): Hr is NOT in LDS -- each lane streams its two Hr columns
 // from the L2-resident workspace into the Newton-matrix registers once per iteration, which
 // keeps the footprint small enough for two waves per SIMD.  Small batches (every wavefront
@@ -189,18 +156,18 @@ struct Dims {
 template <class D, bool HRL>
 struct IpmLayout {
   static constexpr int NY = D::NY, NU = D::NU, NC = D::NC, NB = D::NB;
-  static constexpr int I_G = D::W_G, I_U = D::W_U;
+  static constexpr int I_G = D::W_G;
   static constexpr int I_HR = D::W_HR;                 // valid when HRL
   static constexpr int STAGE = HRL ? D::W_X : D::W_HR; // workspace prefix copied to LDS
   static constexpr int I_VY = STAGE;                   // y (current iterate)
   static constexpr int I_VY2 = I_VY + even(NY);        // search direction
-  static constexpr int I_UV = I_VY2 + even(NY);        // U_y v for the torque rows
+  static constexpr int I_UV = I_VY2 + even(NY);        // (unused slot: keeps the layout fixed)
   static constexpr int I_VR = I_UV + even(NU);         // a row-space vector
   static constexpr int I_DR = I_VR + D::NRL * kRow;    // lambda / s
   static constexpr int I_MASK = I_DR + D::NRL * kRow;
   static constexpr int I_TAU = I_MASK + even(NC);
   static constexpr int I_XB = I_TAU + even(NU);
-  static constexpr int I_DINV = I_XB + even(D::NXR);      // 1/D of the factorization (32)
+  static constexpr int I_DINV = I_XB + even(D::NV);       // 1/D of the factorization (32)
   static constexpr int IL = I_DINV + 2 * kRow;
 };
 template <class D>
@@ -478,16 +445,9 @@ __device__ __forceinline__ double bcast_guarded(double v) {
 }
 
 // ============================ kernel 1: reduced QP per env ==================================
-// Dense products of the assembly (2 A'WA, H_dv X, X'(H_dv X)) on the FP64 matrix cores
-// (v_mfma_f64_16x16x4f64) for torque-coordinate models; OSC_SETUP_MFMA=0 builds the VALU 2x2-tile
-// form for A/B.
+// Dense products of the assembly (H_dv X, X'(H_dv X), and 2 A'WA where it fits one tile) on the
+// FP64 matrix cores (v_mfma_f64_16x16x4f64).
 typedef double d4 __attribute__((ext_vector_type(4)));
-template <class D>
-constexpr bool kSetupMfma = D::MF;
-// Ha on MFMA: forced by bit 1, else where [J e] fits one 16-column block (WaLTER: NA = 15, one
-// tile over 102 task rows, phase B 10.9k -> 8.9k clocks per wave; Go2's NA = 19 pads to 32)
-template <class D>
-constexpr bool kHaMfma = D::HAM;
 
 // The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
 // of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
@@ -509,11 +469,8 @@ __device__ __forceinline__ void setup_env(
   double* sC = sm + D::O_C;
   double* sHa = sm + D::O_HA;
   double* sX = sm + D::O_X;
-  double* sU = D::TY ? sm + D::O_X + NB * NY1P : sm + D::O_U;   // TY: U parked in X's last rows
+  double* sU = sm + D::O_X + NB * NY1P;   // U parked in X's last rows until X replaces it
   double* sMask = sm + D::O_MASK;
-  double* sT1 = sm + D::O_T1;
-  double* sHr = sm + D::O_HR;
-  double* sG = sm + D::O_G;
 
   STAMP_DECL
   STAMP_BEGIN();
@@ -586,7 +543,7 @@ __device__ __forceinline__ void setup_env(
   // H_dv = 2 J'WJ + 2 w_reg I,  f_dv = 2 J'W (b - t)   (autogen.py:131-238, 304-319)
   // One 2x2 tile of the upper triangle per lane (column pairs read as one 16-byte LDS load);
   // each entry (i <= j) accumulates fma(w_r A_ri, A_rj) over r in order.
-  // (torque coordinates: H_dv and f_dv also go to the workspace from here, no write phase)
+  // (H_dv and f_dv also go to the workspace from here, no write phase)
   double* const wha = ws + static_cast<size_t>(env) * D::WS;
   auto put_ha = [&](int i, int j, double v) {
     if (i >= NA || j >= NA) return;
@@ -594,16 +551,14 @@ __device__ __forceinline__ void setup_env(
     if (i == j && i < NV) v += 2.0 * P->w_reg;
     sHa[i * NA + j] = v;
     sHa[j * NA + i] = v;
-    if constexpr (D::TY && OSC_WS_DIRECT) {
-      if (j < NV) {                          // H_dv (i <= j < NV), both triangles
-        wha[D::W_HD + i * NV + j] = v;
-        wha[D::W_HD + j * NV + i] = v;
-      } else if (j == NV && i < NV) {        // f_dv = the [J e] Gram's last column
-        wha[D::W_GD + i] = v;
-      }
+    if (j < NV) {                          // H_dv (i <= j < NV), both triangles
+      wha[D::W_HD + i * NV + j] = v;
+      wha[D::W_HD + j * NV + i] = v;
+    } else if (j == NV && i < NV) {        // f_dv = the [J e] Gram's last column
+      wha[D::W_GD + i] = v;
     }
   };
-  if constexpr (kHaMfma<D>) {
+  if constexpr (D::JG) {
     // FP64 MFMA (v_mfma_f64_16x16x4f64): 16x16 tiles of the upper block triangle, K = task rows
     // in steps of 4.  Lane l feeds row/column (l & 15) of a block at k-row 4q + (l >> 4) and
     // gets back C[(l >> 4) + 4 r][l & 15] (tools/mb_mfma64.hip checks this layout on the GPU).
@@ -623,18 +578,13 @@ __device__ __forceinline__ void setup_env(
       for (int u = 0; u < CH; ++u) {
         const int r = 4 * (q0 + u) + lg;
         const bool rv = r < S;
-        wv[u] = rv ? (D::JG ? sA[D::O_W + r] : P->w_row[r]) : 0.0;
+        wv[u] = rv ? sA[D::O_W + r] : 0.0;
 #pragma unroll
         for (int b = 0; b < NBK; ++b) {
           const int col = 16 * b + lc;
-          if constexpr (D::JG) {
-            // [J | e | 0] row r: J from the fragments loaded in phase A, e from LDS
-            const double ev = sA[D::O_E + (rv ? r : 0)];
-            v[u][b] = !rv ? 0.0 : (col < NV ? jf[q0 + u < KSJ ? q0 + u : 0] : (col == NV ? ev : 0.0));
-          } else {
-            const double x = sA[(rv ? r : 0) * NAP + (col < NAP ? col : 0)];
-            v[u][b] = (rv && col < NAP) ? x : 0.0;
-          }
+          // [J | e | 0] row r: J from the fragments loaded in phase A, e from LDS
+          const double ev = sA[D::O_E + (rv ? r : 0)];
+          v[u][b] = !rv ? 0.0 : (col < NV ? jf[q0 + u < KSJ ? q0 + u : 0] : (col == NV ? ev : 0.0));
         }
       }
 #pragma unroll
@@ -762,7 +712,7 @@ __device__ __forceinline__ void setup_env(
       if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = 0.0;
   }
   wave_sync();
-  if constexpr (D::TY) {
+  {
     // y = (u, z): X = M^-1 [B | Jc | -C] over all NV rows by block elimination on the base block.
     // The code above left X_b = M_bb^-1 [-M_ba | Jc_b | -C_b] in rows 0..NB-1 and
     // U = M_ab X_b + [M_aa | -Jc_a | C_a] in rows NB.. of sX; U's first NU columns are the Schur
@@ -775,7 +725,7 @@ __device__ __forceinline__ void setup_env(
     // lane c of any row solves column c and takes L's entries from the row's lane k by DPP --
     // so the factor never goes through LDS.  Every lane runs every step (a DPP read needs its
     // source lane active); lanes past the last column compute garbage and write zeros.
-    static_assert(NU <= kRow, "TY: S fits one 16-lane row");
+    static_assert(NU <= kRow, "S fits one 16-lane row");
     STAMP_END(2);
     STAMP_BEGIN();
     const int lj = lane & (kRow - 1);
@@ -853,13 +803,13 @@ __device__ __forceinline__ void setup_env(
       for (int r = 0; r < NB; ++r) {
         const double v = live ? xb[r] : 0.0;
         sX[r * NY1P + c] = v;
-        if (OSC_WS_DIRECT) wx[r * NY1P + c] = v;
+        wx[r * NY1P + c] = v;
       }
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
         const double v = live ? xa[i] : 0.0;
         sX[(NB + i) * NY1P + c] = v;
-        if (OSC_WS_DIRECT) wx[(NB + i) * NY1P + c] = v;
+        wx[(NB + i) * NY1P + c] = v;
       }
     }
     wave_sync();
@@ -871,25 +821,13 @@ __device__ __forceinline__ void setup_env(
   STAMP_END(2);
   STAMP_BEGIN();
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
-  // dv = Pm [y;1] with Pm = [X ; (I_nu 0 0)],  T1 = H_dv Pm (+ f_dv in the affine column),
-  // Hr = Pm' T1 + 2 (w_tau + w_reg) U'U + 2 w_reg I_z,   g = last column.
-  // T1 = H_dv Pm: one 2x2 tile (rows r0, r0+1 x columns c0, c0+1) per lane and round.
-  // (TY: Pm = X, no identity rows; the affine column still carries f_dv)
-  auto t1_base = [&](int r, int c) -> double {
-    if constexpr (D::TY) {
-      const double v = sHa[r * NA + NV];
-      return c == NY ? v : 0.0;
-    } else {
-      const double v = sHa[r * NA + ((c < NU) ? NB + c : NV)];   // read unconditionally
-      return (c < NU || c == NY) ? v : 0.0;
-    }
-  };
-  if constexpr (kSetupMfma<D>) {
-    // FP64 MFMA, torque coordinates: T1 = H_dv X (+ f_dv in the affine column) as 16x16 tiles
+  // Hr = X' T1 + 2 (w_tau + w_reg) I_u + 2 w_reg I_z,  g = last column,  T1 = H_dv X (+ f_dv in
+  // the affine column).
+  {
+    // FP64 MFMA: T1 = H_dv X (+ f_dv in the affine column) as 16x16 tiles
     // kept in registers, then [Hr | g] = X' T1 with T1's registers as the B operand -- register
     // r of a T1 tile holds rows (l >> 4) + 4 r, exactly the k-rows of one 4-step -- so T1 never
     // goes through LDS.  X's fragments serve both products (B of the first, A of the second).
-    static_assert(D::TY && D::NXR == NV, "MFMA setup: torque coordinates");
     constexpr int RB = (NV + 15) / 16, CB = (NY1P + 15) / 16, KS = (NV + 3) / 4;
     const int lc = lane & 15, lg = lane >> 4;
     double xf[KS][CB];   // X[4q + lg][16 cb + lc]
@@ -931,7 +869,7 @@ __device__ __forceinline__ void setup_env(
           t1[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(hf[rb][q], xf[q][cb], t1[rb][cb], 0, 0, 0);
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
-    double* wsv = ws + static_cast<size_t>(env) * D::WS;   // JG: [Hr | g] out from registers
+    double* wsv = ws + static_cast<size_t>(env) * D::WS;   // [Hr | g] out from registers
     constexpr int NT = CB * (CB + 1) / 2;   // upper block triangle, tiles interleaved per k-step
     d4 hacc[NT];
 #pragma unroll
@@ -962,147 +900,33 @@ __device__ __forceinline__ void setup_env(
             if (b < NY) {
               if (a == b && a < NU) v += wu2;
               if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
-              if constexpr (D::HRD) {
-                wsv[D::W_HR + a * NY + b] = v;
-                wsv[D::W_HR + b * NY + a] = v;
-              } else {
-                sHr[a * NY + b] = v;
-                sHr[b * NY + a] = v;
-              }
+              wsv[D::W_HR + a * NY + b] = v;
+              wsv[D::W_HR + b * NY + a] = v;
             } else {
-              if constexpr (D::HRD) wsv[D::W_G + a] = v;
-              else sG[a] = v;
+              wsv[D::W_G + a] = v;
             }
           }
         }
       }
     wave_sync();
-  } else {
-  for (int p = lane; p < D::NBT; p += kWave) {
-    const int r0 = 2 * (p / D::NY2), c0 = 2 * (p % D::NY2);
-    double t00 = t1_base(r0, c0), t01 = t1_base(r0, c0 + 1);
-    double t10 = t1_base(r0 + 1, c0), t11 = t1_base(r0 + 1, c0 + 1);
-#pragma unroll 6
-    for (int i = 0; i < D::NXR; ++i) {
-      const double h0 = sHa[r0 * NA + i], h1 = sHa[(r0 + 1) * NA + i];
-      const double2 x = *reinterpret_cast<const double2*>(sX + i * NY1P + c0);
-      t00 = fma(h0, x.x, t00);
-      t01 = fma(h0, x.y, t01);
-      t10 = fma(h1, x.x, t10);
-      t11 = fma(h1, x.y, t11);
-    }
-    *reinterpret_cast<double2*>(sT1 + r0 * NY1P + c0) = make_double2(t00, t01);
-    *reinterpret_cast<double2*>(sT1 + (r0 + 1) * NY1P + c0) = make_double2(t10, t11);
-  }
-  wave_sync();
-  STAMP_END(3);
-  STAMP_BEGIN();
-  {
-    // Hr | g = Pm' T1 + 2 (w_tau + w_reg) U'U (+ 2 w_reg I_z): one 2x2 tile of the upper
-    // triangle per lane and round; each entry (a <= b) accumulates X[r][a] T1[r][b] and
-    // U[q][a] U[q][b] in order.
-    const double wu2 = 2.0 * (P->w_torque + P->w_reg);
-    const double wr2 = 2.0 * P->w_reg;
-    auto put_hr = [&](int a, int b, double acc) {
-      const int kz = (a >= NU) ? (a - NU) / 3 : 0;
-      const double mk = sMask[kz < NC ? kz : NC - 1];      // read before any branch
-      if (b >= NY1 || (a == NY && b == NY)) return;
-      if (b < NY) {
-        if (D::TY && a == b && a < NU) acc += wu2;   // TY: U'U = I_nu
-        if (a == b && a >= NU) {
-          acc += wr2;
-          if (mk == 0.0) acc = 1.0;   // pinned z: identity row
-        }
-        sHr[a * NY + b] = acc;
-        sHr[b * NY + a] = acc;
-      } else {
-        sG[a] = acc;
-      }
-    };
-    for (int p = lane; p < D::NBH; p += kWave) {
-      int a0, b0;
-      upper_pair<D::NY2>(p, a0, b0);
-      a0 *= 2;
-      b0 *= 2;
-      double h[2][2], uu[2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const double t1 = sT1[(NB + ((a0 + i < NU) ? a0 + i : NU - 1)) * NY1P + b0 + j];
-          h[i][j] = (!D::TY && a0 + i < NU) ? t1 : 0.0;
-          uu[i][j] = 0.0;
-        }
-#pragma unroll 6
-      for (int r = 0; r < D::NXR; ++r) {
-        const double2 xa = *reinterpret_cast<const double2*>(sX + r * NY1P + a0);
-        const double2 tb = *reinterpret_cast<const double2*>(sT1 + r * NY1P + b0);
-        h[0][0] = fma(xa.x, tb.x, h[0][0]);
-        h[0][1] = fma(xa.x, tb.y, h[0][1]);
-        h[1][0] = fma(xa.y, tb.x, h[1][0]);
-        h[1][1] = fma(xa.y, tb.y, h[1][1]);
-      }
-#pragma unroll
-      for (int q = 0; q < (D::TY ? 0 : NU); ++q) {
-        const double2 ua = *reinterpret_cast<const double2*>(sU + q * NY1P + a0);
-        const double2 ub = *reinterpret_cast<const double2*>(sU + q * NY1P + b0);
-        uu[0][0] = fma(ua.x, ub.x, uu[0][0]);
-        uu[0][1] = fma(ua.x, ub.y, uu[0][1]);
-        uu[1][0] = fma(ua.y, ub.x, uu[1][0]);
-        uu[1][1] = fma(ua.y, ub.y, uu[1][1]);
-      }
-      put_hr(a0, b0, fma(wu2, uu[0][0], h[0][0]));
-      put_hr(a0, b0 + 1, fma(wu2, uu[0][1], h[0][1]));
-      if (a0 != b0) put_hr(a0 + 1, b0, fma(wu2, uu[1][0], h[1][0]));
-      put_hr(a0 + 1, b0 + 1, fma(wu2, uu[1][1], h[1][1]));
-    }
-  }
-  wave_sync();
   }
 
   STAMP_END(4);
   STAMP_BEGIN();
-  // ---------------- write the reduced QP: workspace [Hr | g | U | X] -------------------------
-  double* w = ws + static_cast<size_t>(env) * D::WS;
-  if constexpr (!D::HRD) {   // (HRD: written from phase D's registers)
-    for (int i = lane; i < NY * NY; i += kWave) w[D::W_HR + i] = sHr[i];
-    for (int i = lane; i < NY; i += kWave) w[D::W_G + i] = sG[i];
-  }
-  for (int i = lane; i < D::NUW * NY1P; i += kWave) w[D::W_U + i] = sU[i];
-  if (!D::TY || !OSC_WS_DIRECT) {   // (torque coordinates: X, H_dv, f_dv written where formed)
-    for (int i = lane; i < D::NXR * NY1P; i += kWave) w[D::W_X + i] = sX[i];
-  }
-  if constexpr (D::TY && !OSC_WS_DIRECT) {
-    for (int i = lane; i < NV * NV; i += kWave) w[D::W_HD + i] = sHa[(i / NV) * NA + i % NV];
-    for (int i = lane; i < NV; i += kWave) w[D::W_GD + i] = sHa[i * NA + NV];
-  }
+  // (X, H_dv, f_dv and [Hr | g] were stored to the workspace where they were formed)
   STAMP_END(5);
   STAMP_STORE_SETUP();
 }
 
-// XCD-aware env order of the assembly grid.  Blocks are dealt round-robin over the 8 XCDs
-// (block b and b + 8 share one; MI355X_MICROARCH.md), and interior-point block w (envs 4w..4w+3)
-// runs on XCD w % 8, so setup block b takes an env of an interior-point block on its own XCD:
-// the reduced QP the interior point reads right after is then in that XCD's L2 rather than
-// another XCD's.  A bijection on [0, nenv) when nenv is a multiple of 32, identity otherwise.
-#ifndef OSC_SETUP_XCD
-#define OSC_SETUP_XCD 0   // A/B: no measurable change (Go2 4,096 0.1819 vs 0.1815 ms)
-#endif
-__device__ __forceinline__ int setup_env_of_block(int b, int nenv) {
-  if (!OSC_SETUP_XCD || (nenv & 31) != 0) return b;
-  const int x = b & 7, m = b >> 3;                  // XCD, index among its blocks
-  const int w = 8 * (m >> 2) + x;                   // interior-point block on XCD x
-  return 4 * w + (m & 3);
-}
-
+// The assembly grid maps block b to env b: an XCD-aware order that put each env's assembly on
+// the XCD of its interior-point block measured no change (Go2 4,096 0.1819 vs 0.1815 ms).
 template <class D>
 __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
   __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
-  setup_env<D>(P, setup_env_of_block(static_cast<int>(blockIdx.x), nenv), nenv, gM, gC, gJ, gb, gT,
-               gmask, ws, sm);
+  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm);
 }
 
 // One model's arguments to a two-model launch.
@@ -1145,16 +969,6 @@ __device__ __forceinline__ void fmac_bcast2(double& a, double& b, double src, do
                  : "+v"(a), "+v"(b) : "v"(src), "v"(ma), "v"(mb), "n"(K));
 }
 
-// (a_i, b_i) += bcast_{i%16}(i < 16 ? x0 : x1) * (ma, mb)_i for i < N: the row group's
-// distributed vector x (x0 = x[lane], x1 = x[lane+16]) times lane-local columns.
-template <int N>
-__device__ __forceinline__ void rank1_rows(double (&a)[N], double (&b)[N], double x0, double x1,
-                                           double ma, double mb) {
-  static_for<0, N>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    fmac_bcast2<i % kRow, i % kRow == 0>(a[i], b[i], i < kRow ? x0 : x1, ma, mb);
-  });
-}
 template <int N>
 __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double x1,
                                          const double (&ma)[N], const double (&mb)[N]) {
@@ -1182,614 +996,11 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // (one ds_write instead of a lane select), each lane reads its own two back at the end.
 // Slot-1 lanes past N (N < 32) hold a copy of column N-1 (the caller loads jj1 = N-1 there);
 // they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
-// finite, and never a broadcast source.
-// ==================== kernel 1b: reduced QP, four environments per wavefront ================
-// Torque coordinates only.  The interior point's mapping: one 16-lane DPP row per environment,
-// so every serial step (base-block LDL^T, the Schur complement's factorisation and solves) is
-// done once per env instead of once per lane or per row of a 64-lane wave, and the whole batch
-// is resident at once at one wave per SIMD (4,096 envs on 1,024 SIMDs: one round, where the
-// 64-lane kernel needs two at two waves per SIMD).  Same closed forms as setup_env; the sums run
-// in another order (J's rows are staged contact rows last), so results agree to rounding.
-// LDS per env (doubles); regions are reused phase by phase:
-//   stage   A = [J | e | 0] (S x NAP, rows in slot order) | M | C
-//   Ha      H_dv | f_dv over A's rows (A is dead once every lane holds its Ha tiles)
-//   X       X_b / U, then X (NV x NY1P) after H_dv | f_dv
-//   T1      H_dv X (+ f_dv in the affine column) after X
-//   out     g | Hr (the interior point's LDS layout) over H_dv | f_dv | X
-// An opaque 0 that depends on v: LDS addresses offset by it cannot be issued before v exists
-// (bounds the loads in flight where the compiler would otherwise hoist a whole unrolled loop's).
-__device__ __forceinline__ unsigned after(double v) {
-  unsigned z = 0;
-  asm volatile("" : "+v"(z) : "v"(v));
-  return z;
-}
-
-template <class D>
-struct Setup4Lds {
-  static constexpr int NV = D::NV, NY1P = D::NY1P;
-  static constexpr int A = 0;
-  static constexpr int M = A + D::S * D::NAP;
-  static constexpr int C = M + NV * NV;
-  static constexpr int JC = C + even(NV);            // unscaled Jc rows (3 NC x NV) + a dump pair
-  static constexpr int STAGE_END = JC + 3 * D::NC * NV + 2;
-  static constexpr int H = 0;
-  static constexpr int F = H + NV * NV;
-  static constexpr int X = F + even(NV);
-  static constexpr int T1 = X + NV * NY1P;
-  static constexpr int END = T1 + NV * NY1P;
-  static constexpr int SIZE = even(cmax(STAGE_END, END));
-  static constexpr int OUT = even(D::NY) + even(D::NY * D::NY);   // g | Hr
-  static_assert(OUT <= X + NV * NY1P || OUT <= SIZE, "g | Hr fits the region");
-};
-template <class D>
-constexpr bool setup4_fits() {   // four envs per wave in one SIMD's share of a CU's LDS (40 KB)
-  return D::TY && D::NU <= kRow && D::NY1 <= 2 * kRow && D::NV <= 2 * kRow &&
-         Setup4Lds<D>::SIZE * kEnvPerWave * 8 <= 160 * 1024 / 4;
-}
-// Task row staged in LDS slot s: the rows that are not contact translational rows first, then
-// the 3 NC contact rows in order -- Jc's rows end up in one contiguous block.
-template <class D>
-constexpr int setup4_row_of_slot(int s) {
-  constexpr int JC0 = 3 * (D::NS - D::NC), NZ = 3 * D::NC;
-  return s < D::S - NZ ? (s < JC0 ? s : s + NZ) : JC0 + (s - (D::S - NZ));
-}
-template <class D>
-constexpr int setup4_slot_of_row(int r) {
-  constexpr int JC0 = 3 * (D::NS - D::NC), NZ = 3 * D::NC;
-  return r < JC0 ? r : (r < JC0 + NZ ? D::S - NZ + (r - JC0) : r - NZ);
-}
-
-// One wavefront's four environments (envs 4 blk + grp).  `sm` holds kEnvPerWave regions of
-// `stride` doubles; on return each env's region starts with its g | Hr (interior-point layout)
-// and the workspace holds X | H_dv | f_dv (refinement, outputs).  Rows of envs past nenv replay
-// env nenv - 1 and write nothing.
-template <class D>
-__device__ __forceinline__ void setup_rows(
-    const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gM,
-    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
-    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
-    double* __restrict__ sm, int stride) {
-  using L4 = Setup4Lds<D>;
-  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
-                NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NAP = D::NAP, NZ = 3 * NC;
-  static_assert(D::TY && NV % 2 == 0 && NY1P % 2 == 0 && NAP == NV + 2, "setup_rows layout");
-  const int lane = threadIdx.x;
-  const int grp = lane / kRow, l = lane % kRow;
-  const int env_raw = blk * kEnvPerWave + grp;
-  const bool valid = env_raw < nenv;
-  const int env = valid ? env_raw : nenv - 1;
-  double* E = sm + grp * stride;
-  double* sA = E + L4::A;
-  double* sM = E + L4::M;
-  double* sC = E + L4::C;
-  double* wsenv = ws + static_cast<size_t>(env) * D::WS;
-  STAMP_DECL
-  STAMP_BEGIN();
-
-  // ---------------- stage: every load in flight first ----------------
-  // A = W^1/2 [J | e | 0]: Ha = 2 A'A needs no weight inside its row loop
-  Batch2<S * NV / 2, kRow> bJ;
-  double wsq[Batch2<S * NV / 2, kRow>::T];
-#pragma unroll
-  for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
-    const int c = l + t * kRow;
-    wsq[t] = P->w_sqrt[(c < S * NV / 2 ? c : S * NV / 2 - 1) / (NV / 2)];
-  }
-  Batch2<NV * NV / 2, kRow> bM;
-  Batch2<NV / 2, kRow> bC;
-  bJ.load(gJ + static_cast<size_t>(env) * S * NV, l);
-  bM.load(gM + static_cast<size_t>(env) * NV * NV, l);
-  bC.load(gC + static_cast<size_t>(env) * NV, l);
-  double mk[NC];
-#pragma unroll
-  for (int k = 0; k < NC; ++k) mk[k] = gmask[static_cast<size_t>(env) * NC + k];
-  constexpr int TE = (S + kRow - 1) / kRow;
-  double eb[TE], et[TE], ew[TE];
-#pragma unroll
-  for (int q = 0; q < TE; ++q) {
-    const int r = (l + q * kRow < S) ? l + q * kRow : S - 1;
-    const int half = r / (3 * NS), rr = r % (3 * NS);
-    ew[q] = P->w_sqrt[r];
-    eb[q] = gb[static_cast<size_t>(env) * S + r];
-    et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
-  }
-  // contact rows also unscaled (X_b, U need Jc itself); other chunks to the dump pair
-  {
-    constexpr int JC0 = 3 * (NS - NC);
-    double2* jc2 = reinterpret_cast<double2*>(E + L4::JC);
-#pragma unroll
-    for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
-      const int c = l + t * kRow;
-      const int cc = c < S * NV / 2 ? c : S * NV / 2 - 1;
-      const int rc = cc / (NV / 2) - JC0;
-      const bool in = rc >= 0 && rc < NZ;
-      jc2[in ? rc * (NV / 2) + cc % (NV / 2) : NZ * NV / 2] = bJ.v[t];
-    }
-  }
-  // J row r -> A row setup4_slot_of_row(r), 16-byte chunks (NV / 2 per row), scaled by sqrt(w_r)
-#pragma unroll
-  for (int t = 0; t < Batch2<S * NV / 2, kRow>::T; ++t) {
-    bJ.v[t].x *= wsq[t];
-    bJ.v[t].y *= wsq[t];
-  }
-  bJ.store(sA, l, [](int c) {
-    const int r = c / (NV / 2);
-    return setup4_slot_of_row<D>(r) * (NAP / 2) + c % (NV / 2);
-  });
-  bM.store(sM, l);
-  bC.store(sC, l);
-#pragma unroll
-  for (int q = 0; q < TE; ++q) {   // e = b - t and the zero pad column (lanes past S rewrite row S-1)
-    const int r = (l + q * kRow < S) ? l + q * kRow : S - 1;
-    const int sl = setup4_slot_of_row<D>(r);
-    *reinterpret_cast<double2*>(sA + sl * NAP + NV) = make_double2((eb[q] - et[q]) * ew[q], 0.0);
-  }
-  wave_sync();
-
-  STAMP_END(0);
-  STAMP_BEGIN();
-  // ---------------- Ha = 2 [J e]' W [J e] (upper 2x2 tiles; the e.e corner is not needed) --------
-  constexpr int NA2 = NAP / 2;
-  constexpr int NTA = NA2 * (NA2 + 1) / 2 - 1;
-  constexpr int TA = (NTA + kRow - 1) / kRow;
-  // rows outer, the lane's TA tiles inner: TA x 2 loads and TA x 4 accumulators live at a time
-  int hi0[TA], hj0[TA];
-#pragma unroll
-  for (int t = 0; t < TA; ++t) {
-    upper_pair<NA2>((l + t * kRow < NTA) ? l + t * kRow : NTA - 1, hi0[t], hj0[t]);
-    hi0[t] *= 2;
-    hj0[t] *= 2;
-  }
-  double ha[TA][4];
-#pragma unroll
-  for (int t = 0; t < TA; ++t) ha[t][0] = ha[t][1] = ha[t][2] = ha[t][3] = 0.0;
-  // software-pipelined: row s + 1's reads are issued before row s's FMAs
-  double2 hx[TA], hy[TA];
-#pragma unroll
-  for (int t = 0; t < TA; ++t) {
-    hx[t] = *reinterpret_cast<const double2*>(sA + hi0[t]);
-    hy[t] = *reinterpret_cast<const double2*>(sA + hj0[t]);
-  }
-#pragma unroll 2
-  for (int s = 0; s < S; ++s) {
-    const double* an = sA + (s + 1 < S ? s + 1 : s) * NAP;
-    double2 nx[TA], ny[TA];
-#pragma unroll
-    for (int t = 0; t < TA; ++t) {
-      nx[t] = *reinterpret_cast<const double2*>(an + hi0[t]);
-      ny[t] = *reinterpret_cast<const double2*>(an + hj0[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < TA; ++t) {
-      ha[t][0] = fma(hx[t].x, hy[t].x, ha[t][0]);
-      ha[t][1] = fma(hx[t].x, hy[t].y, ha[t][1]);
-      ha[t][2] = fma(hx[t].y, hy[t].x, ha[t][2]);
-      ha[t][3] = fma(hx[t].y, hy[t].y, ha[t][3]);
-      hx[t] = nx[t];
-      hy[t] = ny[t];
-    }
-  }
-  wave_sync();   // A is dead: H_dv | f_dv take its place
-  double* sH = E + L4::H;
-  double* sF = E + L4::F;
-  {
-    // branch-free scatter: every entry goes somewhere; the ones not wanted (pad column, the
-    // mirrored half of a diagonal tile) to a slot X overwrites later
-    const double wr2 = 2.0 * P->w_reg;
-    double* dump = E + L4::X + l;   // one slot per lane: a shared one serialises the stores
-    auto put = [&](int i, int j, bool keep, double v) {
-      const bool hj = keep && j < NV, fj = keep && j == NV;
-      v = 2.0 * v + ((i == j) ? wr2 : 0.0);
-      double* p1 = hj ? sH + i * NV + j : (fj ? sF + i : dump);
-      double* p2 = hj ? sH + j * NV + i : dump;
-      *p1 = v;
-      *p2 = v;
-    };
-#pragma unroll
-    for (int t = 0; t < TA; ++t) {
-      const bool ok = l + t * kRow < NTA;
-      const int i0 = hi0[t], j0 = hj0[t];
-      put(i0, j0, ok, ha[t][0]);
-      put(i0, j0 + 1, ok, ha[t][1]);
-      put(i0 + 1, j0, ok && i0 != j0, ha[t][2]);
-      put(i0 + 1, j0 + 1, ok, ha[t][3]);
-    }
-  }
-  wave_sync();
-
-  STAMP_END(1);
-  STAMP_BEGIN();
-  // ---------------- X_b = M_bb^-1 [-M_ba | Jc_b | -C_b], U = M_ab X_b + [M_aa | -Jc_a | C_a] ----
-  // Lane l: columns c = l and l + 16 of [y; 1] (padding column and past it: zeros).  The base
-  // block's LDL^T is formed per lane (NB^3 / 6 flops) from broadcast LDS reads of M.
-  double xbs[2][NB], us[2][NU];
-  {
-    double Lb[NB][NB];
-    double dinv[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j <= i; ++j) Lb[i][j] = sM[i * NV + j];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      dinv[k] = recip1(Lb[k][k]);
-#pragma unroll
-      for (int i = k + 1; i < NB; ++i) {
-        const double lik = Lb[i][k] * dinv[k];
-#pragma unroll
-        for (int j = k + 1; j <= i; ++j) Lb[i][j] = fma(-lik, Lb[j][k], Lb[i][j]);
-      }
-#pragma unroll
-      for (int i = k + 1; i < NB; ++i) Lb[i][k] *= dinv[k];
-    }
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int c = l + kRow * sl;
-      const bool cu = c < NU, cz = !cu && c < NY, live = c < NY1;
-      const int kz = cz ? (c - NU) / 3 : 0;
-      double mkz = mk[0];
-#pragma unroll
-      for (int k = 1; k < NC; ++k) mkz = (kz == k) ? mk[k] : mkz;
-      const bool pinned = cz && mkz == 0.0;
-      const int cc = live ? c : NY;   // a readable column for lanes that write zeros
-      const bool ccu = cc < NU, ccz = !ccu && cc < NY;
-      const double* sJc = E + L4::JC;
-      const double* xp = ccu ? sM + NB + cc : (ccz ? sJc + (cc - NU) * NV : sC);
-      const int xs = ccu ? NV : 1;
-      const double xsg = ccz ? 1.0 : -1.0;
-      const double* up = ccu ? sM + NB * NV + NB + cc : (ccz ? sJc + (cc - NU) * NV + NB : sC + NB);
-      const double usg = ccz ? -1.0 : 1.0;
-      double x[NB];
-#pragma unroll
-      for (int i = 0; i < NB; ++i) x[i] = (pinned || !live) ? 0.0 : xsg * xp[i * xs];
-#pragma unroll
-      for (int k = 0; k < NB; ++k)
-#pragma unroll
-        for (int i = k + 1; i < NB; ++i) x[i] = fma(-Lb[i][k], x[k], x[i]);
-#pragma unroll
-      for (int k = 0; k < NB; ++k) x[k] *= dinv[k];
-#pragma unroll
-      for (int k = NB - 1; k >= 0; --k)
-#pragma unroll
-        for (int i = 0; i < k; ++i) x[i] = fma(-Lb[k][i], x[k], x[i]);
-#pragma unroll
-      for (int i = 0; i < NB; ++i) xbs[sl][i] = x[i];
-#pragma unroll
-      for (int a = 0; a < NU; ++a) {
-        double acc = (pinned || !live) ? 0.0 : usg * up[a * xs];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
-        us[sl][a] = acc;
-      }
-    }
-  }
-  wave_sync();   // M, C and Jc are dead: X_b | U into X's rows
-  double* sX = E + L4::X;
-#pragma unroll
-  for (int sl = 0; sl < 2; ++sl) {
-    const int c = l + kRow * sl;
-    if (c < NY1P) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = xbs[sl][i];
-#pragma unroll
-      for (int a = 0; a < NU; ++a) sX[(NB + a) * NY1P + c] = us[sl][a];
-    }
-  }
-  wave_sync();
-
-  STAMP_END(2);
-  STAMP_BEGIN();
-  // ---------------- Schur complement S = U[:, :NU] = L D L' in the env's row; X = [x_b; x_a] -----
-  {
-    double col[NU];
-    const int lj = l < NU ? l : 0;
-#pragma unroll
-    for (int i = 0; i < NU; ++i) col[i] = sX[(NB + i) * NY1P + lj];
-    double dj = 1.0;
-    static_for<0, NU>([&](auto K) {
-      constexpr int k = decltype(K)::value;
-      const double rk = recip1(bcast_guarded<k>(col[k]));
-      if (l == k) dj = rk;
-      const double m = (l > k) ? -col[k] * rk : 0.0;
-      static_for<k + 1, NU>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        fmac_bcast_self<k, true>(col[i], m);
-      });
-    });
-    double dinv[NU];
-    static_for<0, NU>([&](auto K) {
-      constexpr int k = decltype(K)::value;
-      dinv[k] = bcast_guarded<k>(dj);
-    });
-    double xa0[NU], xa1[NU], xb0[NB], xb1[NB], xbc[NB];
-    {
-      const int c0 = l, c1 = l + kRow;
-      const int r0 = c0 < NY1 ? c0 : NY, r1 = c1 < NY1 ? c1 : NY;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        const double u0 = sX[(NB + i) * NY1P + r0], u1 = sX[(NB + i) * NY1P + r1];
-        xa0[i] = (c0 < NU) ? ((i == c0) ? 1.0 : 0.0) : -u0;
-        xa1[i] = (c1 < NU) ? ((i == c1) ? 1.0 : 0.0) : -u1;
-      }
-#pragma unroll
-      for (int r = 0; r < NB; ++r) {
-        xb0[r] = (c0 < NU) ? 0.0 : sX[r * NY1P + r0];
-        xb1[r] = (c1 < NU) ? 0.0 : sX[r * NY1P + r1];
-        xbc[r] = sX[r * NY1P + lj];   // X_b[:, j]: the DPP source of lane j
-      }
-    }
-    static_for<0, NU>([&](auto K) {   // L z = r
-      constexpr int k = decltype(K)::value;
-      const double t0 = -xa0[k] * dinv[k], t1 = -xa1[k] * dinv[k];
-      static_for<k + 1, NU>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        fmac_bcast2<k, false>(xa0[i], xa1[i], col[i], t0, t1);
-      });
-    });
-#pragma unroll
-    for (int k = 0; k < NU; ++k) {
-      xa0[k] *= dinv[k];
-      xa1[k] *= dinv[k];
-    }
-    static_for<0, NU - 1>([&](auto J) {   // L' x = y
-      constexpr int i = NU - 2 - decltype(J)::value;
-      double a0 = 0.0, a1 = 0.0;
-      static_for<i + 1, NU>([&](auto K) {
-        constexpr int k = decltype(K)::value;
-        fmac_bcast2<i, false>(a0, a1, col[k], xa0[k], xa1[k]);
-      });
-      xa0[i] = fma(-dinv[i], a0, xa0[i]);
-      xa1[i] = fma(-dinv[i], a1, xa1[i]);
-    });
-    static_for<0, NU>([&](auto Q) {   // x_b += X_b[:, :NU] x_a
-      constexpr int q = decltype(Q)::value;
-#pragma unroll
-      for (int r = 0; r < NB; ++r) fmac_bcast2<q, false>(xb0[r], xb1[r], xbc[r], xa0[q], xa1[q]);
-    });
-    wave_sync();   // every lane has read X_b and U
-    const int c0 = l, c1 = l + kRow;
-#pragma unroll
-    for (int r = 0; r < NB; ++r) {
-      sX[r * NY1P + c0] = c0 < NY1 ? xb0[r] : 0.0;
-      if (c1 < NY1P) sX[r * NY1P + c1] = c1 < NY1 ? xb1[r] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      sX[(NB + i) * NY1P + c0] = c0 < NY1 ? xa0[i] : 0.0;
-      if (c1 < NY1P) sX[(NB + i) * NY1P + c1] = c1 < NY1 ? xa1[i] : 0.0;
-    }
-  }
-  wave_sync();
-  STAMP_END(3);
-  STAMP_BEGIN();
-  // X and H_dv | f_dv -> workspace (refinement, outputs), coalesced
-  if (valid) {
-    static_assert(D::W_GD == D::W_HD + NV * NV && L4::F == L4::H + NV * NV, "H_dv | f_dv blocks");
-    constexpr int NX2 = NV * NY1P / 2, NH2 = (NV * NV + NV) / 2;
-    const double2* sx2 = reinterpret_cast<const double2*>(sX);
-    const double2* sh2 = reinterpret_cast<const double2*>(sH);
-    double2* wx2 = reinterpret_cast<double2*>(wsenv + D::W_X);
-    double2* wh2 = reinterpret_cast<double2*>(wsenv + D::W_HD);
-    for (int i = l; i < NX2; i += kRow) wx2[i] = sx2[i];
-    for (int i = l; i < NH2; i += kRow) wh2[i] = sh2[i];
-  }
-
-  STAMP_END(4);
-  STAMP_BEGIN();
-  // ---------------- T1 = H_dv X (+ f_dv in the affine column): 2x2 tiles --------------------
-  double* sT1 = E + L4::T1;
-  {
-    constexpr int NY2 = NY1P / 2, NR2 = NV / 2;
-    constexpr int NT = NR2 * NY2;
-    constexpr int TT = (NT + kRow - 1) / kRow;
-    int tr0[TT], tc0[TT];
-    double tt[TT][4];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) {
-      const int p = (l + t * kRow < NT) ? l + t * kRow : NT - 1;
-      tr0[t] = 2 * (p / NY2);
-      tc0[t] = 2 * (p % NY2);
-      const bool aff = tc0[t] == NY;   // affine column: T1 starts at f_dv
-      tt[t][0] = aff ? sF[tr0[t]] : 0.0;
-      tt[t][1] = 0.0;
-      tt[t][2] = aff ? sF[tr0[t] + 1] : 0.0;
-      tt[t][3] = 0.0;
-    }
-    // software-pipelined over i (H entries as column pairs: one 16-byte read per two i)
-    double2 ch0[TT], ch1[TT], cx0[TT], cx1[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) {
-      ch0[t] = *reinterpret_cast<const double2*>(sH + tr0[t] * NV);
-      ch1[t] = *reinterpret_cast<const double2*>(sH + (tr0[t] + 1) * NV);
-      cx0[t] = *reinterpret_cast<const double2*>(sX + tc0[t]);
-      cx1[t] = *reinterpret_cast<const double2*>(sX + NY1P + tc0[t]);
-    }
-#pragma unroll 1
-    for (int i = 0; i < NV; i += 2) {
-      const int in = i + 2 < NV ? i + 2 : i;
-      double2 nh0[TT], nh1[TT], nx0[TT], nx1[TT];
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        nh0[t] = *reinterpret_cast<const double2*>(sH + tr0[t] * NV + in);
-        nh1[t] = *reinterpret_cast<const double2*>(sH + (tr0[t] + 1) * NV + in);
-        nx0[t] = *reinterpret_cast<const double2*>(sX + in * NY1P + tc0[t]);
-        nx1[t] = *reinterpret_cast<const double2*>(sX + (in + 1) * NY1P + tc0[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        tt[t][0] = fma(ch0[t].x, cx0[t].x, tt[t][0]);
-        tt[t][1] = fma(ch0[t].x, cx0[t].y, tt[t][1]);
-        tt[t][2] = fma(ch1[t].x, cx0[t].x, tt[t][2]);
-        tt[t][3] = fma(ch1[t].x, cx0[t].y, tt[t][3]);
-        tt[t][0] = fma(ch0[t].y, cx1[t].x, tt[t][0]);
-        tt[t][1] = fma(ch0[t].y, cx1[t].y, tt[t][1]);
-        tt[t][2] = fma(ch1[t].y, cx1[t].x, tt[t][2]);
-        tt[t][3] = fma(ch1[t].y, cx1[t].y, tt[t][3]);
-        ch0[t] = nh0[t];
-        ch1[t] = nh1[t];
-        cx0[t] = nx0[t];
-        cx1[t] = nx1[t];
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < TT; ++t) {
-      if (l + t * kRow >= NT) continue;
-      *reinterpret_cast<double2*>(sT1 + tr0[t] * NY1P + tc0[t]) = make_double2(tt[t][0], tt[t][1]);
-      *reinterpret_cast<double2*>(sT1 + (tr0[t] + 1) * NY1P + tc0[t]) =
-          make_double2(tt[t][2], tt[t][3]);
-    }
-  }
-  wave_sync();
-
-  STAMP_END(5);
-  STAMP_BEGIN();
-  // ---------------- Hr | g = X' T1 + 2 (w_tau + w_reg) I_u + 2 w_reg I_z (upper 2x2 tiles) ------
-  constexpr int NY2 = NY1P / 2;
-  constexpr int NTH = NY2 * (NY2 + 1) / 2;
-  constexpr int TH = (NTH + kRow - 1) / kRow;
-  int ha0[TH], hb0[TH];
-#pragma unroll
-  for (int t = 0; t < TH; ++t) {
-    upper_pair<NY2>((l + t * kRow < NTH) ? l + t * kRow : NTH - 1, ha0[t], hb0[t]);
-    ha0[t] *= 2;
-    hb0[t] *= 2;
-  }
-  double hr[TH][4];
-#pragma unroll
-  for (int t = 0; t < TH; ++t) hr[t][0] = hr[t][1] = hr[t][2] = hr[t][3] = 0.0;
-  double2 qx[TH], qt[TH];
-#pragma unroll
-  for (int t = 0; t < TH; ++t) {
-    qx[t] = *reinterpret_cast<const double2*>(sX + ha0[t]);
-    qt[t] = *reinterpret_cast<const double2*>(sT1 + hb0[t]);
-  }
-#pragma unroll 2
-  for (int r = 0; r < NV; ++r) {
-    const int rn = r + 1 < NV ? r + 1 : r;
-    double2 nx[TH], nt[TH];
-#pragma unroll
-    for (int t = 0; t < TH; ++t) {
-      nx[t] = *reinterpret_cast<const double2*>(sX + rn * NY1P + ha0[t]);
-      nt[t] = *reinterpret_cast<const double2*>(sT1 + rn * NY1P + hb0[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < TH; ++t) {
-      hr[t][0] = fma(qx[t].x, qt[t].x, hr[t][0]);
-      hr[t][1] = fma(qx[t].x, qt[t].y, hr[t][1]);
-      hr[t][2] = fma(qx[t].y, qt[t].x, hr[t][2]);
-      hr[t][3] = fma(qx[t].y, qt[t].y, hr[t][3]);
-      qx[t] = nx[t];
-      qt[t] = nt[t];
-    }
-  }
-  STAMP_END(6);
-  STAMP_BEGIN();
-  wave_sync();   // X and T1 are dead: g | Hr in the interior point's layout
-  {
-    double* sG = E;
-    double* sHr = E + even(NY);
-    double* dump = E + L4::T1 + l;   // T1 is dead here; one slot per lane
-    const double wu2 = 2.0 * (P->w_torque + P->w_reg);
-    const double wr2 = 2.0 * P->w_reg;
-    // z diagonal of a pinned contact: identity row (its X column is zero)
-    auto put = [&](int a, int b, bool keep, double acc) {
-      const bool hb = keep && b < NY, gb_ = keep && b == NY && a < NY;
-      const int kz = (a - NU) / 3;
-      double m = mk[0];
-#pragma unroll
-      for (int k = 1; k < NC; ++k) m = (kz == k) ? mk[k] : m;
-      const bool dg = a == b;
-      acc += dg ? ((a < NU) ? wu2 : wr2) : 0.0;
-      acc = (dg && a >= NU && m == 0.0) ? 1.0 : acc;
-      double* p1 = hb ? sHr + a * NY + b : (gb_ ? sG + a : dump);
-      double* p2 = hb ? sHr + b * NY + a : dump;
-      *p1 = acc;
-      *p2 = acc;
-    };
-#pragma unroll
-    for (int t = 0; t < TH; ++t) {
-      const bool ok = l + t * kRow < NTH;
-      const int a0 = ha0[t], b0 = hb0[t];
-      put(a0, b0, ok, hr[t][0]);
-      put(a0, b0 + 1, ok, hr[t][1]);
-      put(a0 + 1, b0, ok && a0 != b0, hr[t][2]);
-      put(a0 + 1, b0 + 1, ok, hr[t][3]);
-    }
-  }
-  wave_sync();
-  STAMP_END(7);
-  STAMP_STORE_SETUP();
-}
-
-// Standalone form: g | Hr copied from LDS to the workspace (the interior-point kernels read the
-// same layout as osc_setup_kernel writes).
-template <class D>
-__global__ __launch_bounds__(kWave, 1) void osc_setup4_kernel(
-    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
-    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
-    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
-  static_assert(setup4_fits<D>(), "setup_rows LDS budget");
-  __shared__ __attribute__((aligned(16))) double sm[kEnvPerWave * Setup4Lds<D>::SIZE];
-  const int blk = static_cast<int>(blockIdx.x);
-  setup_rows<D>(P, blk, nenv, gM, gC, gJ, gb, gT, gmask, ws, sm, Setup4Lds<D>::SIZE);
-  const int grp = threadIdx.x / kRow, l = threadIdx.x % kRow;
-  const int env = blk * kEnvPerWave + grp;
-  if (env < nenv) {
-    constexpr int N2 = (even(D::NY) + even(D::NY * D::NY)) / 2;
-    static_assert(D::W_G == 0 && D::W_HR == even(D::NY), "g | Hr workspace prefix");
-    const double2* s2 = reinterpret_cast<const double2*>(sm + grp * Setup4Lds<D>::SIZE);
-    double2* w2 = reinterpret_cast<double2*>(ws + static_cast<size_t>(env) * D::WS);
-    for (int i = l; i < N2; i += kRow) w2[i] = s2[i];
-  }
-}
-
-#ifndef OSC_LDL_OVERLAP
-#define OSC_LDL_OVERLAP 0   // measured ~1 % slower at Go2 4,096 (tools/ab_run.sh)
-#endif
+// finite, and never a broadcast source.  (Issuing pivot k+1's broadcast and reciprocal inside
+// step k's trailing update measured ~1 % slower at Go2 4,096.)
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
-#if OSC_LDL_OVERLAP
-  // Pivot k + 1 is final once step k has updated row k + 1 (its first FMA pair), so its
-  // broadcast, reciprocal and multipliers are issued right there and overlap the rest of step
-  // k's trailing update instead of waiting behind it (a lone wave otherwise stalls ~8 dependent
-  // f64 latencies per pivot).  Same operations, same order per value: bitwise-identical factor.
-  auto prep = [&](auto kc, double& t0, double& t1) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int s = k / kRow, kl = k % kRow;
-    const double own = (s == 0) ? c0[k] : c1[k];
-    const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
-    const double inv = recip1(dk);
-    sdinv[k] = inv;
-    t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(-c0[k] * inv);
-    constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
-    t1 = keep_lanes<rows_mask(kT1)>(-c1[k] * inv);
-  };
-  double t0n, t1n;
-  prep(std::integral_constant<int, 0>{}, t0n, t1n);
-  static_for<0, N>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int s = k / kRow, kl = k % kRow;
-    const double t0 = t0n, t1 = t1n;
-    auto upd = [&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      // the first update of a step reads a row the previous step may have written only a
-      // couple of instructions earlier (late pivots): guarded
-      constexpr bool kNop = (i == k + 1);
-      if constexpr (s == 0) {
-        fmac_bcast<kl, kNop>(c1[i], c0[i], t1);
-        if constexpr (k < kRow - 1) fmac_bcast_self<kl>(c0[i], t0);
-      } else {
-        fmac_bcast_self<kl, kNop>(c1[i], t1);
-      }
-    };
-    if constexpr (k + 1 < N) {
-      upd(std::integral_constant<int, k + 1>{});
-      prep(std::integral_constant<int, k + 1>{}, t0n, t1n);
-      static_for<k + 2, N>(upd);
-    }
-  });
-#else
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
@@ -1815,7 +1026,6 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
       }
     });
   });
-#endif
   wave_sync();
   dinv0 = sdinv[l];
   dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
@@ -1883,27 +1093,12 @@ struct RefineLds {
   static constexpr int GD = HD + D::NV * D::NV;
   static constexpr int SIZE = GD + even(D::NV);   // = W_SOL - W_X in the workspace
 };
-// Refinement modes of the IPM body: none (the interior point alone; a torque-coordinate model
-// then hands its result to osc_refine_kernel through W_SOL), the refinement pass alone
-// (osc_refine_kernel), or both in one wavefront (one-wave variant: no hand-off, no second launch).
+// Refinement modes of the IPM body: none (the interior point alone, handing its result to
+// osc_refine_kernel through W_SOL: warm-started solves past one wave per SIMD, whose fused kernel
+// spills, and models created with OSC_REFINE_STEPS=0), the refinement pass alone
+// (osc_refine_kernel), or both in one wavefront (every cold solve and the one-wave warm solve:
+// no hand-off, no second launch).
 constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
-// setup_rows (four envs per wavefront, one round at 4,096 envs) measured no faster than the
-// 64-lane osc_setup_kernel (Go2 4,096: 35.3 vs 33.7 us): off by default
-#ifndef OSC_SETUP4
-#define OSC_SETUP4 0
-#endif
-#ifndef OSC_FUSE_REFINE
-#define OSC_FUSE_REFINE 1
-#endif
-#ifndef OSC_HR_REG
-#define OSC_HR_REG 1
-#endif
-#ifndef OSC_FUSE_REFINE_LARGE   // the two-wave variant runs the refinement too (no second kernel)
-#define OSC_FUSE_REFINE_LARGE 1
-#endif
-#ifndef OSC_FUSE_REFINE_WARM    // so do the warm-started solve's two passes
-#define OSC_FUSE_REFINE_WARM 1
-#endif
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
@@ -1913,34 +1108,20 @@ constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's itera
 // assembled (registers hold it from then on) and only keeps [H_dv | f_dv] apart.
 template <class D, bool SMALL, int RF>
 constexpr int refine_lds_extra() {
-  if constexpr (RF == kRfNone || !D::TY) return 0;
+  if constexpr (RF == kRfNone) return 0;
   else if constexpr (RF == kRfFused && !SMALL) return 0;   // reads [X | H_dv | f_dv] from L2
   else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())   // (DMA: whole 1 KB rows)
-    return OSC_HD_DMA ? (((RefineLds<D>::SIZE - RefineLds<D>::HD) / 2 + kWave - 1) / kWave) * kWave * 2
-                      : RefineLds<D>::SIZE - RefineLds<D>::HD;
+    return (((RefineLds<D>::SIZE - RefineLds<D>::HD) / 2 + kWave - 1) / kWave) * kWave * 2;
   else return RefineLds<D>::SIZE;
 }
-// Two-wave variant: minimum LDS request in doubles (0 = its own need).  A larger request caps
-// the wavefronts resident per CU, and with them the Hr working set each XCD's L2 must hold
-#ifndef OSC_LARGE_LDS_MIN
-#define OSC_LARGE_LDS_MIN 0
-#endif
-// Two-wave variant: Hr's upper triangle packed in LDS (row i at i NY - i (i - 1) / 2; 300 doubles
-// per Go2 env, 9.6 KB per wavefront beside its 7.9 KB: still two waves per SIMD) instead of each
-// lane re-reading its two Hr columns from the workspace every iteration
-#ifndef OSC_HR_PACKED
-#define OSC_HR_PACKED 0
-#endif
-template <class D, bool SMALL, int RF>
-constexpr int hr_packed_lds() {   // doubles per env
-  return (OSC_HR_PACKED && !SMALL && RF != kRfOnly) ? even(D::NY * (D::NY + 1) / 2) : 0;
-}
+// Two-wave variant, measured and not adopted: capping the waves resident per CU so
+// each XCD's Hr working set fits its L2 (slower: the eighth wave per CU hides issue latency), and
+// Hr's upper triangle packed in LDS (2.5 % slower: at full occupancy the Hr loads' latency is
+// already hidden, and the packed addressing costs issue slots).
 template <class D, bool SMALL, int RF = kRfNone>
 constexpr int ipm_lds_doubles() {
-  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>() +
-                     hr_packed_lds<D, SMALL, RF>();
-  return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2)
-               : cmax(kEnvPerWave * il, OSC_LARGE_LDS_MIN);
+  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>();
+  return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
 }
 
 // The body of one IPM wavefront (envs 4 blk .. 4 blk + 3); `sm` is its ipm_lds_doubles<D, SMALL>
@@ -1953,11 +1134,10 @@ __device__ __forceinline__ void ipm_block(
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
     int fixup, double* __restrict__ sm) {
-  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NB = D::NB, NY = D::NY, NY1P = D::NY1P,
-                MI = D::MI, NRL = D::NRL;
-  constexpr int RF = D::TY ? RF_ : kRfNone;   // refinement exists in torque coordinates only
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NY = D::NY, NY1P = D::NY1P, MI = D::MI,
+                NRL = D::NRL;
+  constexpr int RF = RF_;
   constexpr bool REFINE = RF == kRfOnly;      // the refinement pass alone (no interior point)
-  if constexpr (RF_ == kRfOnly && !D::TY) return;
   constexpr bool HRL = ipm_hrl<D, SMALL, RF>();
   using LY = IpmLayout<D, HRL>;
   const int lane = threadIdx.x;
@@ -1974,10 +1154,8 @@ __device__ __forceinline__ void ipm_block(
     write_out = valid && (!fixup || redo);
   }
 
-  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>() + hr_packed_lds<D, SMALL, RF>();
+  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>();
   double* B = sm + grp * kEnvLds;
-  constexpr bool kHrPk = hr_packed_lds<D, SMALL, RF>() > 0;
-  double* sHp = B + LY::IL + refine_lds_extra<D, SMALL, RF>();   // packed Hr (kHrPk)
   // refinement: [X | H_dv | f_dv] of this env; a fused pass with Hr in LDS keeps X in Hr's region
   constexpr bool kXinHr = RF == kRfFused && HRL;
   double* sRX = kXinHr ? B + LY::I_HR : B + LY::IL + RefineLds<D>::X;
@@ -1995,10 +1173,8 @@ __device__ __forceinline__ void ipm_block(
   const unsigned lane_off = static_cast<unsigned>(env - blk * kEnvPerWave) *
                             static_cast<unsigned>(D::WS);
   double* sG = B + LY::I_G;
-  double* sU = B + LY::I_U;
   double* sVy = B + LY::I_VY;
   double* sVy2 = B + LY::I_VY2;
-  double* sUv = B + LY::I_UV;
   double* sVr = B + LY::I_VR;
   double* sDr = B + LY::I_DR;
   double* sMask = B + LY::I_MASK;
@@ -2007,44 +1183,23 @@ __device__ __forceinline__ void ipm_block(
 
   STAMP_DECL
   STAMP_BEGIN();
-  // stage [g | U (| Hr)] (the workspace prefix has the LDS layout) and the mask: all loads in
+  // stage [g (| Hr)] (the workspace prefix has the LDS layout) and the mask: all loads in
   // flight before the first LDS store
   static_assert(LY::STAGE % 2 == 0 && NC <= kRow, "staging layout");
   {
     Batch2<LY::STAGE / 2, kRow> bs;
     bs.load(ws + static_cast<size_t>(env) * D::WS, l);
     const double mk = gmask[static_cast<size_t>(env) * NC + (l < NC ? l : 0)];
-    if constexpr (RF == kRfFused && !kRefG && !(kXinHr && OSC_HD_DMA)) {
-      // the refinement's own LDS block is free all along: its [X | H_dv | f_dv] (HRL:
-      // [H_dv | f_dv]; X takes Hr's region later) is staged now, in the same memory latency
-      // (by DMA instead, the allocator spills the one-wave Go2 kernel to scratch)
-      constexpr int kFrom = kXinHr ? RefineLds<D>::HD : 0;
-      static_assert((RefineLds<D>::SIZE - kFrom) % 2 == 0 && (D::W_X + kFrom) % 2 == 0,
-                    "16-byte staging");
-      Batch2<(RefineLds<D>::SIZE - kFrom) / 2, kRow> bx;
-      bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X + kFrom, l);
-      bx.store(kXinHr ? sRH : sRX, l);
+    if constexpr (RF == kRfFused && !kRefG && !kXinHr) {
+      // the refinement's own LDS block is free all along: its [X | H_dv | f_dv] is staged now,
+      // in the same memory latency (with Hr in LDS, [H_dv | f_dv] and X come by DMA later instead)
+      static_assert(RefineLds<D>::SIZE % 2 == 0 && D::W_X % 2 == 0, "16-byte staging");
+      Batch2<RefineLds<D>::SIZE / 2, kRow> bx;
+      bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X, l);
+      bx.store(sRX, l);
     }
     bs.store(B, l);
     if (l < NC) sMask[l] = mk;
-  }
-  if constexpr (kHrPk) {
-    // row i of Hr's upper triangle: lane l copies entries j = i + l and i + l + 16
-#pragma unroll
-    for (int i = 0; i < NY; ++i) {
-      constexpr int kS = 2;
-      double v[kS];
-#pragma unroll
-      for (int t = 0; t < kS; ++t) {
-        const int j = i + l + kRow * t;
-        v[t] = wsw[lane_off + static_cast<unsigned>(i * NY + (j < NY ? j : NY - 1))];
-      }
-#pragma unroll
-      for (int t = 0; t < kS; ++t) {
-        const int j = i + l + kRow * t;
-        if (j < NY) sHp[i * NY - i * (i - 1) / 2 + (j - i)] = v[t];
-      }
-    }
   }
   const double* sHr = B + LY::I_HR;
   wave_sync();
@@ -2063,7 +1218,7 @@ __device__ __forceinline__ void ipm_block(
       const double sg = (r & 1) ? -1.0 : 1.0;
       const double bnd = (r & 1) ? P->u_lb[q] : P->u_ub[q];
       act[t] = fabs(bnd) < P->inf_thresh;
-      h[t] = D::TY ? sg * bnd : sg * (bnd - sU[q * NY1P + NY]);   // TY: the row is +-y_q
+      h[t] = sg * bnd;                                     // the row is +-y_q
     } else if (r < MI) {
       const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
       const double m = sMask[k];
@@ -2093,39 +1248,8 @@ __device__ __forceinline__ void ipm_block(
   };
   STAMP_END(0);
 
-  // U_y v for the torque rows (lanes l < NU), result in sUv; caller syncs
-  // the torque lanes' own U rows (loop-invariant) in registers for the one-wave Go2 variant
-  constexpr bool kURowReg = SMALL && !D::TY && NY % 2 == 0 && NY <= 24;
-  double urow[kURowReg ? NY : 1];
-  if constexpr (kURowReg) {
-    const int lr = l < NU ? l : 0;
-#pragma unroll
-    for (int i = 0; i < NY; ++i) urow[i] = sU[lr * NY1P + i];
-  }
-  // (TY: the torque rows read y_q itself, there is no product)
-  auto uv_product = [&](const double* v) {
-    if (!D::TY && l < NU) {
-      double a = 0.0;
-      // reads of v issued before the FMAs.  Measured per system (tools/eps_sweep.py):
-      // Go2 (24 columns) 0.268 -> 0.261 ms; WaLTER (32) slower, its registers are the limit.
-      if constexpr (kURowReg) {
-        double2 x[NY / 2];
-#pragma unroll
-        for (int i = 0; i < NY / 2; ++i) x[i] = *reinterpret_cast<const double2*>(v + 2 * i);
-#pragma unroll
-        for (int i = 0; i < NY / 2; ++i) {
-          a = fma(urow[2 * i], x[i].x, a);
-          a = fma(urow[2 * i + 1], x[i].y, a);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NY; ++i) a = fma(sU[l * NY1P + i], v[i], a);
-      }
-      sUv[l] = a;
-    }
-  };
   // (G v)_r for all row slots at once, branch-free, every read issued first (one-wave variant):
-  // torque rows read U_y v, contact rows read their contact's three force entries.
+  // torque rows read y_q, contact rows read their contact's three force entries.
   auto Gv_all = [&](const double* v, double (&out)[NRL]) {
     double uq[NRL], f0[NRL], f1[NRL], f2[NRL];
 #pragma unroll
@@ -2133,7 +1257,7 @@ __device__ __forceinline__ void ipm_block(
       const int r = l + kRow * t;
       const int q = (r < 2 * NU) ? (r >> 1) : 0;
       const int k = (r >= 2 * NU && r < MI) ? (r - 2 * NU) / 6 : 0;
-      uq[t] = D::TY ? v[q] : sUv[q];
+      uq[t] = v[q];
       f0[t] = v[NU + 3 * k];
       f1[t] = v[NU + 3 * k + 1];
       f2[t] = v[NU + 3 * k + 2];
@@ -2149,12 +1273,12 @@ __device__ __forceinline__ void ipm_block(
       out[t] = !act[t] ? 0.0 : ((r < 2 * NU) ? trow : crow);
     }
   };
-  // (G v)_r for row slot t, given sUv = U_y v
+  // (G v)_r for row slot t
   auto Gv = [&](const double* v, int t) -> double {
     if (!act[t]) return 0.0;
     const int r = l + kRow * t;
     if (r < 2 * NU) {
-      const double uq = D::TY ? v[r >> 1] : sUv[r >> 1];
+      const double uq = v[r >> 1];
       return (r & 1) ? -uq : uq;
     }
     const int k = (r - 2 * NU) / 6, rt = (r - 2 * NU) % 6;
@@ -2187,66 +1311,13 @@ __device__ __forceinline__ void ipm_block(
     const double v = (jc == 0) ? v0 : ((jc == 1) ? v1 : v2);
     return jk >= 0 ? v : 0.0;
   };
-  // this lane's two U columns, loop-invariant, kept in registers (AGPR spill space in SMALL)
-  constexpr bool kUCReg = SMALL && !D::TY;
-  double uc0[kUCReg ? NU : 1], uc1[kUCReg ? NU : 1];
-  if constexpr (kUCReg) {
-#pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      uc0[q] = sU[q * NY1P + j0];
-      uc1[q] = sU[q * NY1P + jj1];
-    }
-  }
   auto GTw2 = [&](const double* w, double& r0, double& r1) {
-    double a0 = 0.0, a1 = 0.0;
-    if constexpr (D::TY) {
-      // torque rows +-e_q: lane j0 < NU picks up w[2 j0] - w[2 j0 + 1]; slot j1 >= 16 > NU is
-      // a contact variable
-      const double2 p = *reinterpret_cast<const double2*>(w + 2 * (j0 < NU ? j0 : 0));
-      const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
-      r0 = (j0 < NU ? p.x - p.y : 0.0) + k0;
-      r1 = k1;
-      (void)a0;
-      (void)a1;
-    } else if constexpr (SMALL) {
-      // one wave per SIMD: latency is exposed, registers are not short (AGPR spill space)
-      double d[NU], u0[NU], u1[NU];
-#pragma unroll
-      for (int q = 0; q < NU; ++q) {
-        const double2 p = *reinterpret_cast<const double2*>(w + 2 * q);   // rows 2q, 2q+1
-        d[q] = p.x - p.y;
-      }
-#pragma unroll
-      for (int q = 0; q < NU; ++q) {
-        u0[q] = uc0[q];
-        u1[q] = uc1[q];
-      }
-      const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
-#pragma unroll
-      for (int q = 0; q < NU; ++q) {
-        a0 = fma(u0[q], d[q], a0);
-        a1 = fma(u1[q], d[q], a1);
-      }
-      r0 = a0 + k0;
-      r1 = a1 + k1;
-    } else {
-      // two waves per SIMD: the other wave hides the latency, registers are the limit
-      // (one slot at a time, branchy contact part: the register-lightest form)
-      auto gtw = [&](int jj, int jk, int jc) -> double {
-        double acc = 0.0;
-#pragma unroll
-        for (int q = 0; q < NU; ++q) acc = fma(sU[q * NY1P + jj], w[2 * q] - w[2 * q + 1], acc);
-        if (jk >= 0) {
-          const double* wk = w + 2 * NU + 6 * jk;
-          if (jc == 0) acc += wk[0] - wk[1] + wk[2] - wk[3];
-          else if (jc == 1) acc += wk[0] + wk[1] - wk[2] - wk[3];
-          else acc += -mu_f * (wk[0] + wk[1] + wk[2] + wk[3]) - wk[4] + wk[5];
-        }
-        return acc;
-      };
-      r0 = gtw(j0, jk0, jc0);
-      r1 = gtw(jj1, jk1, jc1);
-    }
+    // torque rows +-e_q: lane j0 < NU picks up w[2 j0] - w[2 j0 + 1]; slot j1 >= 16 > NU is a
+    // contact variable
+    const double2 p = *reinterpret_cast<const double2*>(w + 2 * (j0 < NU ? j0 : 0));
+    const double k0 = contact_term(w, jk0, jc0), k1 = contact_term(w, jk1, jc1);
+    r0 = (j0 < NU ? p.x - p.y : 0.0) + k0;
+    r1 = k1;
   };
   // contact block column (B[0..2][jc]) of var slot in contact jk, from D = lambda/s
   auto contact_col = [&](int jk, int jc, double& v0, double& v1_, double& v2) {
@@ -2267,7 +1338,7 @@ __device__ __forceinline__ void ipm_block(
   // One-wave variant whose Hr does not fit the LDS (WaLTER: 32 x 32 x 4 envs): the lane's two Hr
   // columns are loaded once and kept in registers across the iterations (the one-wave kernel has
   // 512 of them, AGPRs included) instead of being re-read from L2 every iteration.
-  constexpr bool kHrReg = SMALL && !HRL && OSC_HR_REG;
+  constexpr bool kHrReg = SMALL && !HRL;
   double hr0[kHrReg ? NY : 1], hr1[kHrReg ? NY : 1];
   if constexpr (kHrReg) {
 #pragma unroll
@@ -2292,20 +1363,6 @@ __device__ __forceinline__ void ipm_block(
       for (int i = 0; i < NY; ++i) {
         c0[i] = hr0[i];
         c1[i] = hr1[i];
-      }
-    } else if constexpr (kHrPk) {
-      // Hr[i][j] = packed (min, max): row i's entry j at i NY - i (i - 1) / 2 + j - i.  The
-      // lane's bases are formed here, every time (hidden from loop-invariant hoisting, as the
-      // workspace path's: kept live across the loop they spill)
-      int a0 = j0, a1 = jj1;
-      asm volatile("" : "+v"(a0), "+v"(a1));
-      const double* q0 = sHp + (a0 * NY - a0 * (a0 - 1) / 2 - a0);
-      const double* q1 = sHp + (a1 * NY - a1 * (a1 - 1) / 2 - a1);
-#pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        const int oi = i * NY - i * (i - 1) / 2 - i;
-        c0[i] = (i <= a0) ? sHp[oi + a0] : q0[i];
-        c1[i] = (i <= a1) ? sHp[oi + a1] : q1[i];
       }
     } else {
       unsigned off = lane_off;
@@ -2410,7 +1467,6 @@ __device__ __forceinline__ void ipm_block(
         if (v1) sVy[j1] = y1;
       }
       wave_sync();
-      uv_product(sVy);
       wave_sync();
       if (warm) {
         const double dlt = P->warm_delta;
@@ -2454,10 +1510,7 @@ __device__ __forceinline__ void ipm_block(
       const bool far = row_sum(cr) / fmax(m_act, 1.0) > 1e-6;
       const bool mine = far && !done && it == (warm ? P->warm_restart : P->restart_iter);
       restart = __ballot(mine) != 0;
-      if (restart) {
-        uv_product(sVy);
-        wave_sync();
-      }
+      if (restart) wave_sync();
       if (mine) {
 #pragma unroll
         for (int t = 0; t < NRL; ++t) {
@@ -2473,8 +1526,7 @@ __device__ __forceinline__ void ipm_block(
       for (int t = 0; t < NRL; ++t) cs += act[t] ? s[t] * lam[t] : 0.0;
       mu = row_sum(cs) / fmax(m_act, 1.0);
       const bool fresh = it == 0 || mu <= 1e-6 || restart;
-      if (__ballot(fresh) != 0) {   // wave-uniform: the product uses the whole row's lanes
-        uv_product(sVy);
+      if (__ballot(fresh) != 0) {   // wave-uniform
         wave_sync();
 #pragma unroll
         for (int t = 0; t < NRL; ++t) {
@@ -2513,14 +1565,9 @@ __device__ __forceinline__ void ipm_block(
     if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
     STAMP_END(8);
     STAMP_BEGIN();
-    // U' diag(d) U: per torque row q, rank-1 update with u = U[q][.] broadcast from the lane
-    // holding it (DPP) -- no broadcast LDS reads in the loop.
-    // rolled (I-cache, registers); the next row's three LDS reads are issued one trip ahead
-    // (the sum of the two row weights is formed at use, not at load: adding at load time would
-    // wait for the prefetch at the top of every trip)
-    if constexpr (D::TY) {
-      // TY: G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
-      static_assert(D::NU <= kRow, "TY: torque variables in the first column slot");
+    // G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
+    {
+      static_assert(D::NU <= kRow, "torque variables in the first column slot");
       const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
       const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
       dg0 += du;
@@ -2528,21 +1575,6 @@ __device__ __forceinline__ void ipm_block(
         constexpr int i = decltype(I)::value;
         c0[i] += keep_lanes<rows_mask(1u << i)>(du);
       });
-    } else {
-    double2 dd_n = *reinterpret_cast<const double2*>(sDr);
-    double u0_n = sU[j0], u1_n = sU[jj1];
-#pragma unroll 1
-    for (int q = 0; q < NU; ++q) {
-      const double du = dd_n.x + dd_n.y, u0 = u0_n, u1 = u1_n;
-      const int qn = (q + 1 < NU) ? q + 1 : q;
-      dd_n = *reinterpret_cast<const double2*>(sDr + 2 * qn);
-      u0_n = sU[qn * NY1P + j0];
-      u1_n = sU[qn * NY1P + jj1];
-      const double t0 = du * u0, t1 = du * u1;
-      dg0 = fma(t0, u0, dg0);
-      dg1 = fma(t1, u1, dg1);
-      rank1_rows<NY>(c0, c1, u0, u1, t0, t1);
-    }
     }
     STAMP_END(9);
     STAMP_BEGIN();
@@ -2599,7 +1631,6 @@ __device__ __forceinline__ void ipm_block(
       wave_sync();
       STAMP_END(5);
       STAMP_BEGIN();
-      uv_product(sVy2);
       wave_sync();
       // step to the boundary, division-free: 1 / max(1, max_r(-ds/s), max_r(-dl/lambda))
       double rmax = 1.0;
@@ -2682,7 +1713,7 @@ __device__ __forceinline__ void ipm_block(
 #ifdef OSC_STAMPS
   if constexpr (RF != kRfFused) STAMP_STORE();   // the fused pass stores after its refinement
 #endif
-  if constexpr (D::TY && RF == kRfNone) {   // hand the result to the refinement kernel
+  if constexpr (RF == kRfNone) {   // hand the result to the refinement kernel
     if (write_out) {
       // (the W_SOL block is written here and read by nothing else in this kernel)
       double* sol = const_cast<double*>(ws) + static_cast<size_t>(env) * D::WS + D::W_SOL;
@@ -2710,7 +1741,7 @@ __device__ __forceinline__ void ipm_block(
   // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
   // discarded.
   bool refined = false;
-  if constexpr (D::TY && RF != kRfNone) {
+  if constexpr (RF != kRfNone) {
     const bool mine = valid && st == OSC_SOLVE_OK;
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
@@ -2815,7 +1846,7 @@ __device__ __forceinline__ void ipm_block(
                 (void)c;
 #endif
               });
-              if constexpr (OSC_HD_DMA) {
+              {
                 // [H_dv | f_dv] the same way, into the block's refinement region (not staged with
                 // the prologue's loads: 11 of the 27 MB every wave requests at once at 4,096 envs)
                 constexpr int NCH2 = (RefineLds<D>::SIZE - RefineLds<D>::HD) / 2;
@@ -2950,20 +1981,18 @@ __device__ __forceinline__ void ipm_block(
 #ifdef OSC_STAMPS
   if constexpr (RF == kRfFused) STAMP_STORE();
 #endif
-  // ---------------- outputs: tau = U [y;1];  x = (dv_b, dv_a, u, z) ----------------------
+  // ---------------- outputs: tau = y_u;  x = (dv, u, z) with dv = X [y; 1] -----------------
   if (REFINE && !refined) write_out = false;   // the interior point kernel's outputs stand
   if (l < NU) {
-    double tq = D::TY ? sVy[l] : sU[l * NY1P + NY];
-#pragma unroll
-    for (int i = 0; i < (D::TY ? 0 : NY); ++i) tq = fma(sU[l * NY1P + i], sVy[i], tq);
+    const double tq = sVy[l];
     sTau[l] = tq;
     if (write_out) gtau[static_cast<size_t>(env) * NU + l] = tq;
   }
-  if (gx != nullptr) {   // dv rows not in y: X [y; 1]  (TY: all NV of them, two per lane)
+  if (gx != nullptr) {   // dv = X [y; 1], two rows per lane
 #pragma unroll
-    for (int t = 0; t < (D::NXR + kRow - 1) / kRow; ++t) {
+    for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
       const int rr = l + kRow * t;
-      if (rr < D::NXR) {
+      if (rr < NV) {
         const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + rr * NY1P;
         double xb = xr[NY];
 #pragma unroll
@@ -2982,8 +2011,7 @@ __device__ __forceinline__ void ipm_block(
         const int idx = l + kRow * t;
         if (idx < D::NX) {
           double v;
-          if (idx < D::NXR) v = sXb[idx];
-          else if (idx < NV) v = sVy[idx - NB];
+          if (idx < NV) v = sXb[idx];
           else if (idx < NV + NU) v = sTau[idx - NV];
           else v = sVy[NU + idx - NV - NU];
           gx[static_cast<size_t>(env) * D::NX + idx] = v;
@@ -3050,11 +2078,8 @@ __global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, Pair
                                        B.status, B.iters, nullptr, 0, sm);
 }
 
-using Go2 = Dims<18, 12, 4, 5, true>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites; y = (u, z)
-#ifndef OSC_WALTER_TY
-#define OSC_WALTER_TY 1
-#endif
-using Walter = Dims<14, 8, 8, 17, OSC_WALTER_TY>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
+using Go2 = Dims<18, 12, 4, 5>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites
+using Walter = Dims<14, 8, 8, 17>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
 
 enum KernelId { K_NONE = 0, K_GO2 = 1, K_WALTER = 2 };
 
@@ -3158,8 +2183,7 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   m->desc = d;
   m->kid = kid;
   m->dparams = nullptr;
-  m->refine = hp.refine_steps > 0 &&
-              ((kid == K_GO2 && Go2::TY) || (kid == K_WALTER && Walter::TY));
+  m->refine = hp.refine_steps > 0;
   (void)hipGetDevice(&m->device);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess)
@@ -3219,14 +2243,10 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
               double* x, int32_t* status, int32_t* iters, double* ws, double* warm, hipStream_t s,
               unsigned stages) {
   if (stages & kAssemble) {
-    // four envs per wavefront where its LDS fits (Go2), else one env per wavefront
-    if constexpr (OSC_SETUP4 && setup4_fits<D>())
-      hipLaunchKernelGGL(osc_setup4_kernel<D>,
-                         dim3(static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave)),
-                         dim3(kWave), 0, s, model->dparams, nenv, M, C, J, b, T, mask, ws);
-    else
-      hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0,
-                         s, model->dparams, nenv, M, C, J, b, T, mask, ws);
+    // one env per 64-lane wavefront (four envs per wavefront measured no faster: Go2 4,096
+    // 35.3 vs 33.7 us)
+    hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
+                       model->dparams, nenv, M, C, J, b, T, mask, ws);
   }
   if (stages & kInteriorPoint) {
     // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one
@@ -3238,13 +2258,11 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     if (warm != nullptr && status == nullptr)
       status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
     const bool small = nenv <= model->small_batch_max;
-    // The one-wave cold solve runs the refinement in the same wavefront (kRfFused).
-    const bool fused = OSC_FUSE_REFINE && (small || OSC_FUSE_REFINE_LARGE) && warm == nullptr &&
-                       D::TY && model->refine;
-    // (warm and past one wave per SIMD the fused two-wave kernel spills: Go2 65,536 warm 50.0 ->
-    // 44.5 M solves/s, so that case keeps the separate refinement pass)
-    const bool fused_warm = OSC_FUSE_REFINE_WARM && small && warm != nullptr && D::TY &&
-                            model->refine;
+    // Every cold solve runs the refinement in the same wavefront (kRfFused), and so does the
+    // one-wave warm solve; warm past one wave per SIMD the fused two-wave kernel spills (Go2 65,536
+    // warm 50.0 -> 44.5 M solves/s), so that case keeps the separate refinement pass.
+    const bool fused = warm == nullptr && model->refine;
+    const bool fused_warm = small && warm != nullptr && model->refine;
     if (warm == nullptr) {
       if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
@@ -3275,14 +2293,9 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
                              model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
       }
     }
-    if (D::TY && model->refine && !fused && !fused_warm) {
-      if (small)
-        hipLaunchKernelGGL((osc_refine_kernel<D, true>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x);
-      else
-        hipLaunchKernelGGL((osc_refine_kernel<D, false>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x);
-    }
+    if (model->refine && !fused && !fused_warm)   // (warm, past one wave per SIMD)
+      hipLaunchKernelGGL((osc_refine_kernel<D, false>), dim3(nb), dim3(kWave), 0, s,
+                         model->dparams, nenv, mask, ws, tau, x);
   }
 }
 
@@ -3366,18 +2379,8 @@ void launch_pair(const osc_batch_job& a, const osc_batch_job& b, hipStream_t s) 
     return p;
   };
   const PairArgs A = args(a), B = args(b);
-  if constexpr (OSC_SETUP4 && setup4_fits<DB>() && !setup4_fits<DA>()) {
-    // model B's setup runs four envs per wavefront (its solo launch): the models' setups are two
-    // grids, so each model's reduced QP is bitwise the one of its solo solve
-    hipLaunchKernelGGL(osc_setup_kernel<DA>, dim3(static_cast<unsigned>(a.nenv)), dim3(kWave), 0, s,
-                       A.P, A.nenv, A.M, A.C, A.J, A.b, A.T, A.mask, A.ws);
-    hipLaunchKernelGGL(osc_setup4_kernel<DB>,
-                       dim3(static_cast<unsigned>((b.nenv + kEnvPerWave - 1) / kEnvPerWave)),
-                       dim3(kWave), 0, s, B.P, B.nenv, B.M, B.C, B.J, B.b, B.T, B.mask, B.ws);
-  } else {
-    hipLaunchKernelGGL((osc_setup_pair_kernel<DA, DB>),
-                       dim3(static_cast<unsigned>(a.nenv + b.nenv)), dim3(kWave), 0, s, A, B);
-  }
+  hipLaunchKernelGGL((osc_setup_pair_kernel<DA, DB>),
+                     dim3(static_cast<unsigned>(a.nenv + b.nenv)), dim3(kWave), 0, s, A, B);
   const unsigned nb = static_cast<unsigned>((a.nenv + kEnvPerWave - 1) / kEnvPerWave +
                                             (b.nenv + kEnvPerWave - 1) / kEnvPerWave);
   // one-wave interior point of both models with the refinement in the same wavefront

@@ -1,6 +1,5 @@
 """Diagnostic: per-phase cycles of the setup kernel from the OSC_STAMPS build
-(lib/libosc_batch_stamps.so, or $OSC_STAMPS_LIB): mean over waves and the slowest wave
-(OSC_SETUP4=1: the four-envs-per-wave kernel, Go2).
+(lib/libosc_batch_stamps.so, or $OSC_STAMPS_LIB): mean over waves and the slowest wave.
     python tools/setup_stamps.py [nenv]"""
 import ctypes
 import json
@@ -17,10 +16,8 @@ from osc_amd import _lib  # noqa: E402
 from osc_amd.solver import OSCBatchSolver  # noqa: E402
 from osc_amd.synth import SEED_BASE, generate  # noqa: E402
 
-NAMES = (["stage", "Ha", "X_b, U", "Schur + x", "X, H_dv -> ws", "T1", "Hr tiles", "g | Hr put"]
-         if os.environ.get("OSC_SETUP4") else
-         ["A: stage inputs", "B: Ha = 2[J e]'W[J e]", "C: X, U (base block)", "D1: T1",
-          "D2: Hr | g", "write workspace", "C2 (TY): factor S", "C2: solve", "C2: x_b + write"])
+NAMES = ["A: stage inputs", "B: Ha = 2[J e]'W[J e]", "C: X, U (base block)", "D1: T1",
+         "D2: Hr | g", "write workspace", "C2: factor S", "C2: solve", "C2: x_b + write"]
 SLOTS = 12
 nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 for robot in ["unitree_go2", "walter_sr"]:
@@ -31,7 +28,7 @@ for robot in ["unitree_go2", "walter_sr"]:
     for _ in range(2):
         s.assemble_into(out, *args)
     torch.cuda.synchronize()
-    nw = nenv // 4 if os.environ.get("OSC_SETUP4") and robot == "unitree_go2" else nenv
+    nw = nenv
     buf = (ctypes.c_ulonglong * (nw * SLOTS))()
     L = _lib.lib()
     L.osc_debug_setup_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
