@@ -213,30 +213,36 @@ def tumbling_pipeline(solver, nenv: int, steps: int, warmup: int, seed: int, str
             "mean_contacts_active": float(mask.mean().item() * 8)}
 
 
-def run_mixed(args, world, rank, dev, barrier) -> None:
-    """BASELINE configs[4]: mixed Go2 + WaLTER Sr.  Every rank solves its own shard of
-    --nenv-per-gpu Go2 envs AND --nenv-per-gpu WaLTER envs (4,096 + 4,096 per GPU: 65,536 over 8
-    GPUs) in ONE osc_batch_solve_multi call: one assembly grid and one interior-point grid for
-    both models, WaLTER's wavefronts first so Go2's fill the SIMDs its early finishers free
-    (one kernel instantiation per model, no collective).  --mixed-mode streams /
-    serial run the two models as two osc_batch_solve calls on two streams / one stream instead.
-    A step = both shards solved; value = all envs of all ranks / max-over-ranks time."""
-    from osc_amd.solver import OSCBatchSolver, solve_multi_into
-    nenv = args.nenv_per_gpu
+def run_mixed(args, world, rank, dev, barrier, solver_cls=None, multi_fn=None,
+              nenv=None) -> dict | None:
+    """BASELINE configs[4]: mixed Go2 + WaLTER Sr.  Every rank solves its own shard of `nenv`
+    Go2 envs AND `nenv` WaLTER envs (4,096 + 4,096 per GPU: 65,536 over 8 GPUs) in ONE
+    osc_batch_solve_multi call: one assembly grid and one interior-point grid for both models,
+    WaLTER's wavefronts first so Go2's fill the SIMDs its early finishers free (one
+    kernel instantiation per model, no collective).  --mixed-mode streams / serial run the two
+    models as two osc_batch_solve calls on two streams / one stream instead.  A step = both shards
+    solved; value = all envs of all ranks / max-over-ranks time.  Returns the line on rank 0
+    (the `mixed` object of the headline line, or the line of --robot mixed)."""
+    if solver_cls is None:
+        from osc_amd.solver import OSCBatchSolver as solver_cls
+    if multi_fn is None:
+        from osc_amd.solver import solve_multi_into as multi_fn
+    nenv = args.nenv_per_gpu if nenv is None else nenv
     robots = ("unitree_go2", "walter_sr")
-    main = torch.cuda.current_stream(dev)
-    streams = [torch.cuda.Stream(dev) for _ in robots]
+    clock = DeviceClock(dev)
+    main = clock.stream()
+    streams = [torch.cuda.Stream(dev) for _ in robots] if clock.cuda else [None, None]
     jobs = []
     for i, robot in enumerate(robots):
-        solver = OSCBatchSolver(robot)
+        solver = solver_cls(robot)
         d = generate(robot, nenv, shard_seed(rank) + 500 * i, args.scenario, args.mask)
         jobs.append((solver, solver.prepare(**d), solver.alloc_outputs(nenv)))
     multi_jobs = [(s, o, inp) for s, inp, o in jobs]
 
     def step():
         if args.mixed_mode == "multi":
-            solve_multi_into(multi_jobs, stream=main)
-        elif args.mixed_mode == "serial":
+            multi_fn(multi_jobs, stream=main)
+        elif args.mixed_mode == "serial" or not clock.cuda:
             for solver, inputs, out in jobs:
                 solver.solve_into(out, *inputs, stream=main)
         else:
@@ -248,27 +254,27 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    clock.sync()
+    e0, e1 = clock.event(), clock.event()
     barrier()
-    torch.cuda.synchronize()
+    clock.sync()
     t0 = time.perf_counter()
     e0.record(main)
     for _ in range(args.steps):
         step()
     e1.record(main)
-    torch.cuda.synchronize()
+    clock.sync()
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = e0.elapsed_time(e1) / args.steps
     conv = sum(int((o.status == 0).sum().item()) for _, _, o in jobs)
     stats = reduce_stats(world, dev, 2 * nenv, elapsed, kernel_ms, 0.0, conv)
     if rank != 0:
-        return
+        return None
     value = job_value(stats, args.steps)
     bps = (bytes_per_solve("unitree_go2") + bytes_per_solve("walter_sr")) * nenv
     achieved = bps / (stats.kernel_ms * 1e-3) / 1e9
-    print(json.dumps({
+    return {
         "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": stats.elapsed_s / args.steps * 1e3, "higher_is_better": True,
@@ -287,8 +293,47 @@ def run_mixed(args, world, rank, dev, barrier) -> None:
         "converged_frac": stats.converged,
         **({"rehearsal": f"{os.environ['OSC_DIST_BACKEND']}: {world} ranks on "
                          f"{torch.cuda.device_count()} GPU(s), ranks sharing devices"}
-           if world > 1 and os.environ.get("OSC_DIST_BACKEND", "nccl") != "nccl" else {})}),
-          flush=True)
+           if world > 1 and os.environ.get("OSC_DIST_BACKEND", "nccl") != "nccl" else {})}
+
+
+def run_north_star(args, world, rank, dev, barrier, solver_cls, clock) -> dict | None:
+    """BASELINE.json north_star: Go2 at a GLOBAL batch of --north-star-envs (65,536) split over
+    the N ranks (65,536 / N per GPU: strong scaling of that batch), the same timed-region rules as
+    the headline (warmup, barrier, K cold solves, barrier, max over ranks).  Reported as the
+    `north_star` object of the headline line; the target is >= 1M solves/s on 8 GPUs."""
+    total = args.north_star_envs
+    nenv = total // world + (1 if rank < total % world else 0)
+    solver = solver_cls("unitree_go2")
+    d = generate("unitree_go2", nenv, shard_seed(rank, 5), "standing", "ones")
+    inputs = solver.prepare(**d)
+    out = solver.alloc_outputs(nenv)
+    stream = clock.stream()
+    for _ in range(args.warmup):
+        solver.solve_into(out, *inputs)
+    clock.sync()
+    e0, e1 = clock.event(), clock.event()
+    barrier()
+    clock.sync()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        solver.solve_into(out, *inputs)
+    e1.record(stream)
+    clock.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    conv = int((out.status == 0).sum().item())
+    stats = reduce_stats(world, dev, nenv, elapsed, kernel_ms, 0.0, conv)
+    if rank != 0:
+        return None
+    value = job_value(stats, args.steps)
+    return {"workload": f"unitree_go2 standing, global batch {stats.total_envs} over {world} "
+                        f"GPU(s) ({total // world} per GPU; BASELINE north_star at 8 GPUs)",
+            "global_envs": stats.total_envs, "envs_per_gpu": total // world, "n_gpus": world,
+            "value": value, "unit": "solves/s", "ms_per_step": stats.elapsed_s / args.steps * 1e3,
+            "kernel_ms": stats.kernel_ms, "scaling": "strong (fixed global batch)",
+            "target": 1e6, "meets_target": value >= 1e6, "converged_frac": stats.converged}
 
 
 def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, stream) -> dict:
@@ -415,6 +460,12 @@ def parse_args(argv=None):
                     help="--robot mixed: one osc_batch_solve_multi call, or two solves on two "
                          "streams / on one stream")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--north-star-envs", type=int, default=65536,
+                    help="global Go2 batch of the north_star object (split over the ranks)")
+    ap.add_argument("--no-north-star", action="store_true")
+    ap.add_argument("--mixed-envs", type=int, default=4096,
+                    help="per-model envs per GPU of the mixed (configs[4]) object")
+    ap.add_argument("--no-mixed", action="store_true")
     return ap.parse_args(argv)
 
 
@@ -558,6 +609,22 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
     return line, solver, inputs
 
 
+def attach_multi_gpu_objects(args, world, rank, dev, barrier, solver_cls, clock, line,
+                             multi_fn=None) -> None:
+    """The BASELINE targets beside the headline (every rank takes part; rank 0 attaches them):
+    `north_star` = Go2 at global batch 65,536 split over the ranks, `mixed` = configs[4]'s
+    per-GPU shard (4,096 Go2 + 4,096 WaLTER per rank) through osc_batch_solve_multi."""
+    if not args.no_north_star:
+        ns = run_north_star(args, world, rank, dev, barrier, solver_cls, clock)
+        if line is not None:
+            line["north_star"] = ns
+    if not args.no_mixed:
+        mx = run_mixed(args, world, rank, dev, barrier, solver_cls, multi_fn, args.mixed_envs)
+        if line is not None:
+            line["mixed"] = {k: mx[k] for k in ("value", "unit", "ms_per_step", "converged_frac",
+                                                "config", "roofline")}
+
+
 def single_env(robot: str, ticks: int) -> dict:
     """BASELINE configs[0]: one environment, one tick at a time through the controller
     (osc_amd/bin/osc_tick_latency: OperationalSpaceController::step() = State packing, H2D, GPU
@@ -606,7 +673,9 @@ def main(argv=None) -> None:
         dist_barrier(world)
 
     if args.robot == "mixed":
-        run_mixed(args, world, rank, dev, barrier)
+        line = run_mixed(args, world, rank, dev, barrier)
+        if line is not None:
+            print(json.dumps(line), flush=True)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
@@ -614,6 +683,7 @@ def main(argv=None) -> None:
     from osc_amd.solver import OSCBatchSolver
     clock = DeviceClock(dev)
     line, solver, inputs = run_headline(args, world, rank, dev, barrier, OSCBatchSolver, clock)
+    attach_multi_gpu_objects(args, world, rank, dev, barrier, OSCBatchSolver, clock, line)
     if line is not None:
         nenv = args.nenv_per_gpu
         stream = clock.stream()

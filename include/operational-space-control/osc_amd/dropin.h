@@ -24,6 +24,8 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <filesystem>
 #include <memory>
 #include <string>
@@ -83,12 +85,19 @@ std::vector<double> flat(const M& m) {   // row-major for the RowMajor aliases (
   return std::vector<double>(m.data(), m.data() + m.size());
 }
 
+// The library's vector for an Eigen type: empty before the first solve (the reference's Zero()
+// then), else exactly the type's size -- a mismatch means the header and libosc_controller.so
+// disagree on the robot's dimensions, which must not surface as plausible zero torques.
 template <class M>
 M unflat(const std::vector<double>& v) {
   M m = M::Zero();
-  std::copy(v.begin(), v.begin() + std::min<std::ptrdiff_t>(static_cast<std::ptrdiff_t>(v.size()),
-                                                             static_cast<std::ptrdiff_t>(m.size())),
-            m.data());
+  if (v.empty()) return m;
+  if (static_cast<std::ptrdiff_t>(v.size()) != static_cast<std::ptrdiff_t>(m.size())) {
+    std::fprintf(stderr, "osc_amd::dropin: library returned %zu values for a %td-element type\n",
+                 v.size(), static_cast<std::ptrdiff_t>(m.size()));
+    std::abort();
+  }
+  std::copy(v.begin(), v.end(), m.data());
   return m;
 }
 

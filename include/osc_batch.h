@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define OSC_ABI_VERSION 1
+#define OSC_ABI_VERSION 2
 #define OSC_MAX_SITES 32
 #define OSC_MAX_NU 16
 
@@ -74,7 +74,11 @@ typedef enum {
 typedef enum {
   OSC_SOLVE_OK = 0,               /* converged: complementarity <= eps_mu                     */
   OSC_SOLVE_MAX_ITER = 1,         /* iteration cap reached; best iterate returned             */
-  OSC_SOLVE_NUMERICAL = 2         /* non-finite values encountered (e.g. NaN inputs)         */
+  OSC_SOLVE_NUMERICAL = 2,        /* non-finite values encountered (e.g. NaN inputs)         */
+  OSC_SOLVE_UNREFINED = 3         /* converged (complementarity <= eps_mu) but the full-space
+                                     refinement was rejected: the interior point's iterate is
+                                     returned, accurate only to its stop (~1e-5 normwise at
+                                     eps_mu 1e-9)                               */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C
@@ -94,8 +98,20 @@ typedef struct {
   double z_lb[3];                 /* per-contact force bounds before the mask multiply        */
   double z_ub[3];                 /*   (osc.h:297-308): {-inf,-inf,0} / {inf,inf,big_number}  */
   double infinity;                /* OSQP_INFTY (1e30); |bound| >= infinity/1e10 = no bound   */
-  double eps_mu;                  /* interior-point stop: mean complementarity <= eps_mu      */
+  double eps_mu;                  /* interior-point stop: mean complementarity <= eps_mu;
+                                     models without the refinement stop at min(eps_mu, 1e-12) */
   int32_t max_iter;               /* interior-point iteration cap                             */
+  /* Wheel no-slip equality rows (ABI 2) -- the design walter_sr_wheels/autogen/autogen.py:128-240
+   * leaves commented out, opt-in here.  wheel_rows = 1 adds, for every contact site i (a wheel),
+   *   d_roll_i . (J_p,i dv + b_i) - wheel_radius[i] * dv[wheel_dof[i]] = 0      (longitudinal)
+   *   d_lat_i  . (J_p,i dv + b_i)                                     = 0      (lateral)
+   * with J_p,i / b_i the contact site's translational rows of J / b (the Jacobian-dot bias
+   * J_dot_p,i qd of the design) and the directions d_roll, d_lat per env (osc_solve_extras).
+   * wheel_dof[i] = -1: no rolling term (a model without that wheel joint).  Each wheel's two rows
+   * are multiplied by its contact mask, as the contact-force bounds are (osc.h:492-495). */
+  int32_t wheel_rows;             /* 0 = off (the reference's QP), 1 = on                    */
+  int32_t wheel_dof[OSC_MAX_SITES];
+  double wheel_radius[OSC_MAX_SITES];
 } osc_model_desc;
 
 typedef struct osc_model osc_model;   /* opaque: descriptor + device-resident parameters */
@@ -194,6 +210,33 @@ typedef struct {
  * model's wavefronts fill the SIMDs freed by the first one's iteration-count tail; anything else
  * runs the jobs one after another on `stream`. */
 int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, void* stream);
+
+/* Per-call extras of osc_batch_solve_ex. */
+typedef struct {
+  /* [nenv][nc][6] DEVICE: (d_roll, d_lat) of every wheel; required iff the model has wheel rows */
+  const double* wheel_dir;
+  /* [nenv][osc_dual_rows] DEVICE, nullable: the dual solution in OSQP's convention
+   * (H x + f + A'y = 0, y > 0 on an active upper bound, < 0 on an active lower bound) over the
+   * reference's rows A = [Aeq (dynamics; wheel rows); Aineq; I_n] (operational_space_controller.h:
+   * 483-497) -- the reference's OsqpSolver::dual_solution (osc.h:534-535).  Requires x != NULL. */
+  double* y;
+} osc_solve_extras;
+
+/* Rows of the dual solution: nv (+ 2 nc wheel rows) + 4 nc + (nv + nu + 3 nc). */
+int osc_dual_rows(const osc_model* model, int32_t* rows);
+
+/* osc_batch_solve with the per-call extras (NULL extras = osc_batch_solve).  A model with wheel
+ * rows is solved only through this entry (and osc_batch_assemble_ex + osc_batch_solve_assembled);
+ * its warm-started and multi-model paths return OSC_ERR_UNSUPPORTED_DIMS. */
+int osc_batch_solve_ex(const osc_model* model, int32_t nenv,
+                       const double* M, const double* C, const double* J, const double* b,
+                       const double* T, const double* contact_mask, const osc_solve_extras* extras,
+                       double* tau, double* x, int32_t* status, int32_t* iters,
+                       void* workspace, size_t workspace_bytes, void* stream);
+int osc_batch_assemble_ex(const osc_model* model, int32_t nenv,
+                          const double* M, const double* C, const double* J, const double* b,
+                          const double* T, const double* contact_mask, const double* wheel_dir,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Human-readable name of an osc_status. */
 const char* osc_status_string(int status);

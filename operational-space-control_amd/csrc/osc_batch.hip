@@ -71,7 +71,14 @@ struct DevParams {
   int32_t max_iter;
   int32_t refine_steps;              // full-space refinement steps after the interior point
   double refine_penalty;             // active-row penalty, x max diag(Hr)
-  double w_sqrt[6 * OSC_MAX_SITES];  // sqrt(w_row): setup_rows stages W^1/2 [J | e]
+  double w_sqrt[6 * OSC_MAX_SITES];  // (unused slot: keeps the layout of the fields above)
+  // wheel no-slip rows (models built with them only; walter_sr_wheels/autogen/autogen.py:128-240)
+  int32_t wheel_dof[OSC_MAX_SITES];  // dof of wheel i's joint, -1 = no rolling term
+  double wheel_radius[OSC_MAX_SITES];
+  double wheel_penalty;              // equality-row penalty D_w, x max diag(Hr)
+  double wheel_tol;                  // interior point: |row residual| <= wheel_tol to stop
+  double refine_max_move;            // a refinement moving y by more (relative) is rejected
+  int32_t refine_dual_extra;         // WH with duals requested: this many more refinement steps
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -85,9 +92,12 @@ constexpr int even(int a) { return (a + 1) & ~1; }   // keep LDS/workspace regio
 // 16-column tile (WaLTER, NA = 15); Go2's 19 columns would pad to 32 and stay on exact 2x2 VALU
 // tiles (Go2 4,096: phase B 7.7k vs 3.5k clocks per wave).  X, H_dv, f_dv and [Hr | g] are stored
 // to the workspace where they are formed (no copy-out phase).
-template <int NV_, int NU_, int NC_, int NS_>
+// WH_: the model carries the wheel no-slip equality rows (two per contact wheel).
+template <int NV_, int NU_, int NC_, int NS_, bool WH_ = false>
 struct Dims {
   static constexpr int NV = NV_, NU = NU_, NC = NC_, NS = NS_;
+  static constexpr bool WH = WH_;
+  static constexpr int NW = WH ? 2 * NC : 0;  // wheel no-slip rows
   static constexpr int NB = NV - NU;          // unactuated (floating-base) dofs
   static constexpr int NZ = 3 * NC;
   static constexpr int NY = NU + NZ;          // reduced variables (u, z)
@@ -113,10 +123,16 @@ struct Dims {
   // interior point (its gradient never goes through Hr)
   static constexpr int W_HD = W_X + NV * NY1P;
   static constexpr int W_GD = W_HD + NV * NV;
-  // interior-point result handed to the refinement kernel: [y | q (lambda on rows with
-  // lambda > s, else 0; row slots) | status]
+  // interior-point result handed to the refinement kernel (and, with duals requested, to the
+  // dual kernel): [y | q (lambda on rows with lambda > s, else 0; row slots) | status]
   static constexpr int W_SOL = W_GD + even(NV);
-  static constexpr int WS = W_SOL + even(NY) + NRL * 16 + 2;
+  // wheel rows: their multipliers nu (dual hand-off), the rows in reduced coordinates
+  // A~ = E [X | x0] - [0 | e] with A~ [y; 1] = E dv - e, each row scaled to unit norm (NW x NY1P),
+  // and [D_w, pad, scale s_w (NW)]
+  static constexpr int W_NU = W_SOL + even(NY) + NRL * 16 + 2;
+  static constexpr int W_AW = W_NU + even(NW);
+  static constexpr int W_DW = W_AW + NW * NY1P;
+  static constexpr int WS = WH ? W_DW + 2 + even(NW) : W_NU;
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
   static constexpr int WW_Y = 2;
   static constexpr int WW_L = WW_Y + even(NY);
@@ -141,7 +157,10 @@ struct Dims {
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
   static constexpr int O_MASK = O_X + NV * NY1P;
-  static constexpr int SMEM = O_MASK + even(NC);
+  static constexpr int O_WE = O_MASK + even(NC);          // WH: E (NW x NV) | e (NW)
+  static constexpr int O_WA = O_WE + NW * NV + even(NW);  // WH: A~ (NW x NY1P)
+  static constexpr int SMEM = O_WA + NW * NY1P;
+  static_assert(NW <= kRow, "IPM: one wheel row per lane of the env's row");
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
 
@@ -457,7 +476,7 @@ __device__ __forceinline__ void setup_env(
     const DevParams* __restrict__ P, int env, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
-    double* __restrict__ sm) {
+    double* __restrict__ sm, const double* __restrict__ gwd) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
                 NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NA = D::NA;
   const int lane = threadIdx.x;
@@ -884,6 +903,99 @@ __device__ __forceinline__ void setup_env(
           hacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xf[q][ab], t1[q / 4][bb][q % 4], hacc[t],
                                                          0, 0, 0);
     }
+    if constexpr (D::WH) {
+      // ---- wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240) ----
+      // E dv = e with, for contact wheel i (mask m_i), rows 2i (longitudinal) and 2i + 1 (lateral):
+      //   m_i (d_roll' J_p,i - r_i e_k') dv = -m_i d_roll' b_i,   m_i d_lat' J_p,i dv = -m_i d_lat' b_i
+      // (J_p,i, b_i: the contact site's translational rows of J and b).  In reduced coordinates
+      // A~ [y; 1] = E (X y + x0) - e, i.e. A~ = E [X | x0] - [0 | e], each row scaled to unit norm.
+      // They enter the reduced QP as the penalty D_w A~'A~ on [Hr | g]; the interior point and the
+      // refinement carry their multipliers (proximal method of multipliers).
+      static_assert(D::JG && D::NW % 4 == 0, "wheel rows: contact rows of J staged in LDS");
+      constexpr int NW = D::NW;
+      double* sE = sm + D::O_WE;   // E (NW x NV) | e (NW); later the row scales
+      double* sAw = sm + D::O_WA;  // A~ (NW x NY1P)
+      const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
+      for (int p = lane; p < NW * NV + NW; p += kWave) {
+        const bool rhs = p >= NW * NV;
+        const int w = rhs ? p - NW * NV : p / NV, j = rhs ? 0 : p % NV;
+        const int i = w >> 1, side = w & 1;
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const double dc = wd[i * 6 + side * 3 + c];
+          const double v = rhs ? gb[static_cast<size_t>(env) * S + JC0 + 3 * i + c]
+                               : sA[(3 * i + c) * NAP + j];   // contact row 3 i + c of J
+          acc = fma(dc, v, acc);
+        }
+        if (!rhs && side == 0 && j == P->wheel_dof[i]) acc -= P->wheel_radius[i];
+        const double m = sMask[i];
+        sE[p] = rhs ? -(m * acc) : m * acc;
+      }
+      wave_sync();
+      for (int p = lane; p < NW * NY1P; p += kWave) {
+        const int w = p / NY1P, c = p % NY1P;
+        double acc = (c == NY) ? -sE[NW * NV + w] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) acc = fma(sE[w * NV + j], sX[j * NY1P + c], acc);
+        sAw[p] = acc;   // (X's pad column is 0)
+      }
+      wave_sync();
+      double sc = 0.0;   // 1 / |A~_w| over the y columns (0: a zero row, a wheel off the ground)
+      if (lane < NW) {
+        double nn = 0.0;
+        for (int c = 0; c < NY; ++c) nn = fma(sAw[lane * NY1P + c], sAw[lane * NY1P + c], nn);
+        sc = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
+        sE[lane] = sc;
+      }
+      wave_sync();
+      for (int p = lane; p < NW * NY1P; p += kWave) sAw[p] *= sE[p / NY1P];
+      wave_sync();
+      // D_w = wheel_penalty x the largest diagonal entry of Hr as stored (the refinement's scale)
+      double dmax = 0.0;
+      {
+        int t = 0;
+#pragma unroll
+        for (int ab = 0; ab < CB; ++ab)
+#pragma unroll
+          for (int bb = ab; bb < CB; ++bb, ++t)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int a = 16 * ab + lg + 4 * rr, b = 16 * bb + lc;
+              const int kz = (a >= NU) ? (a - NU) / 3 : 0;
+              const double mk = sMask[kz < NC ? kz : NC - 1];
+              double v = hacc[t][rr] + ((a < NU) ? wu2 : wr2);
+              v = (a >= NU && mk == 0.0) ? 1.0 : v;
+              dmax = (a == b && a < NY) ? fmax(dmax, fabs(v)) : dmax;
+            }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, kWave));
+      const double dw = P->wheel_penalty * dmax;
+      // [Hr | g] += D_w A~'A~ on the FP64 matrix cores (K = the NW rows, four per step)
+#pragma unroll
+      for (int q = 0; q < NW / 4; ++q) {
+        double af[CB];
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          const int col = 16 * cb + lc;
+          const double v = sAw[(4 * q + lg) * NY1P + (col < NY1P ? col : 0)];
+          af[cb] = col < NY1P ? v : 0.0;
+        }
+        int t = 0;
+#pragma unroll
+        for (int ab = 0; ab < CB; ++ab)
+#pragma unroll
+          for (int bb = ab; bb < CB; ++bb, ++t)
+            hacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(dw * af[ab], af[bb], hacc[t], 0, 0, 0);
+      }
+      for (int p = lane; p < NW * NY1P; p += kWave) wsv[D::W_AW + p] = sAw[p];
+      if (lane == 0) {
+        wsv[D::W_DW] = dw;
+        wsv[D::W_DW + 1] = 0.0;
+      }
+      if (lane < NW) wsv[D::W_DW + 2 + lane] = sc;
+    }
     int tt = 0;
 #pragma unroll
     for (int ab = 0; ab < CB; ++ab)
@@ -924,9 +1036,10 @@ template <class D>
 __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
-    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws) {
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
+    const double* __restrict__ gwd) {
   __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
-  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm);
+  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm, gwd);
 }
 
 // One model's arguments to a two-model launch.
@@ -947,9 +1060,9 @@ __global__ __launch_bounds__(kWave, 2) void osc_setup_pair_kernel(PairArgs A, Pa
   __shared__ __attribute__((aligned(16))) double sm[cmax(DA::SMEM, DB::SMEM)];
   const int blk = static_cast<int>(blockIdx.x);
   if (blk < A.nenv)
-    setup_env<DA>(A.P, blk, A.nenv, A.M, A.C, A.J, A.b, A.T, A.mask, A.ws, sm);
+    setup_env<DA>(A.P, blk, A.nenv, A.M, A.C, A.J, A.b, A.T, A.mask, A.ws, sm, nullptr);
   else
-    setup_env<DB>(B.P, blk - A.nenv, B.nenv, B.M, B.C, B.J, B.b, B.T, B.mask, B.ws, sm);
+    setup_env<DB>(B.P, blk - A.nenv, B.nenv, B.M, B.C, B.J, B.b, B.T, B.mask, B.ws, sm, nullptr);
 }
 
 // ============================ kernel 2: interior point, 4 env / wave ========================
@@ -1108,7 +1221,8 @@ constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's itera
 // assembled (registers hold it from then on) and only keeps [H_dv | f_dv] apart.
 template <class D, bool SMALL, int RF>
 constexpr int refine_lds_extra() {
-  if constexpr (RF == kRfNone) return 0;
+  if constexpr (D::WH && RF == kRfFused) return even(D::NW * D::NY1P);   // A~ (reads [X | ..] from L2)
+  else if constexpr (RF == kRfNone) return 0;
   else if constexpr (RF == kRfFused && !SMALL) return 0;   // reads [X | H_dv | f_dv] from L2
   else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())   // (DMA: whole 1 KB rows)
     return (((RefineLds<D>::SIZE - RefineLds<D>::HD) / 2 + kWave - 1) / kWave) * kWave * 2;
@@ -1133,9 +1247,13 @@ __device__ __forceinline__ void ipm_block(
     const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
-    int fixup, double* __restrict__ sm) {
+    int flags, double* __restrict__ sm) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NY = D::NY, NY1P = D::NY1P, MI = D::MI,
                 NRL = D::NRL;
+  // flags: bit 0 = the cold fix-up pass after a warm-started solve, bit 1 = hand the multipliers
+  // to the dual kernel (W_SOL q, W_NU)
+  const bool fixup = (flags & 1) != 0;
+  const bool want_dual = (flags & 2) != 0;
   constexpr int RF = RF_;
   constexpr bool REFINE = RF == kRfOnly;      // the refinement pass alone (no interior point)
   constexpr bool HRL = ipm_hrl<D, SMALL, RF>();
@@ -1164,7 +1282,9 @@ __device__ __forceinline__ void ipm_block(
   // Two-wave variant with the refinement fused: no LDS for [X | H_dv | f_dv] (two waves per SIMD
   // need <= 20 KB per wave), the refinement reads them from the workspace (L2 / Infinity Cache)
   // (the pointers are formed after the interior-point loop: nothing extra lives across it)
-  constexpr bool kRefG = RF == kRfFused && !SMALL;
+  // (so does a model with wheel rows: its LDS block holds the rows A~ instead)
+  constexpr bool kRefG = RF == kRfFused && (!SMALL || D::WH);
+  double* sAw = B + LY::IL;   // WH: A~ (NW x NY1P), row w read by lane w
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -1197,6 +1317,12 @@ __device__ __forceinline__ void ipm_block(
       Batch2<RefineLds<D>::SIZE / 2, kRow> bx;
       bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X, l);
       bx.store(sRX, l);
+    }
+    if constexpr (D::WH && RF == kRfFused) {
+      static_assert(D::W_AW % 2 == 0 && (D::NW * NY1P) % 2 == 0, "16-byte staging");
+      Batch2<D::NW * NY1P / 2, kRow> ba;
+      ba.load(ws + static_cast<size_t>(env) * D::WS + D::W_AW, l);
+      ba.store(sAw, l);
     }
     bs.store(B, l);
     if (l < NC) sMask[l] = mk;
@@ -1333,12 +1459,38 @@ __device__ __forceinline__ void ipm_block(
     v2 = (jc == 0) ? b02 : (jc == 1) ? b12 : b22;
   };
 
+  // Wheel no-slip rows (WH): A~ [y; 1] = 0, each row w = lane w of the env's row.  The reduced
+  // Hessian / gradient already carry the penalty D_w A~'A~ (setup); the interior point adds
+  // A~' c for the multiplier centre c and moves c by D_w A~ [y; 1] after every step (proximal
+  // method of multipliers).
+  constexpr int NW = D::NW;
+  auto aw_rows = [&](const double* v) -> double {   // (A~ [v; 1])_l on lane l < NW, else 0
+    const double* a = sAw + (l < NW ? l : 0) * NY1P;
+    double acc = a[NY];
+#pragma unroll
+    for (int i = 0; i < NY; ++i) acc = fma(a[i], v[i], acc);
+    return l < NW ? acc : 0.0;
+  };
+  auto aw_cols = [&](double v, double& o0, double& o1) {   // (A~' v) at the lane's slots j0, jj1
+    double a0 = 0.0, a1 = 0.0;
+    static_for<0, NW>([&](auto W) {
+      constexpr int w = decltype(W)::value;
+      fmac_bcast2<w, w == 0>(a0, a1, v, sAw[w * NY1P + j0], sAw[w * NY1P + jj1]);
+    });
+    o0 = a0;
+    o1 = a1;
+  };
+  double cw = 0.0, wnu0 = 0.0, wnu1 = 0.0, rwmax = 0.0, dw = 0.0;
+  if constexpr (D::WH && RF == kRfFused)
+    dw = ws[static_cast<size_t>(env) * D::WS + D::W_DW];
+
   double c0[NY], c1[NY];
   double dinv0, dinv1;
   // One-wave variant whose Hr does not fit the LDS (WaLTER: 32 x 32 x 4 envs): the lane's two Hr
   // columns are loaded once and kept in registers across the iterations (the one-wave kernel has
   // 512 of them, AGPRs included) instead of being re-read from L2 every iteration.
-  constexpr bool kHrReg = SMALL && !HRL;
+  // (not with wheel rows: their per-iteration products need the registers; Hr comes from L2)
+  constexpr bool kHrReg = SMALL && !HRL && !D::WH;
   double hr0[kHrReg ? NY : 1], hr1[kHrReg ? NY : 1];
   if constexpr (kHrReg) {
 #pragma unroll
@@ -1534,7 +1686,7 @@ __device__ __forceinline__ void ipm_block(
           rp[t] = fresh ? r : rp[t];
         }
       }
-      if (!done && mu <= P->eps_mu) {
+      if (!done && mu <= P->eps_mu && (!D::WH || rwmax <= P->wheel_tol)) {
         done = true;
         st = OSC_SOLVE_OK;
         it_done = it;
@@ -1561,6 +1713,10 @@ __device__ __forceinline__ void ipm_block(
     GTw2(sVr, rd0, rd1);
     rd0 += g0;
     rd1 += g1;
+    if constexpr (D::WH) {   // + A~' c (the gradient of the augmented Lagrangian)
+      rd0 += wnu0;
+      rd1 += wnu1;
+    }
     double dg0 = hdg0, dg1 = hdg1;
     if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
     STAMP_END(8);
@@ -1708,6 +1864,14 @@ __device__ __forceinline__ void ipm_block(
     if (v1) sVy[j1] = y1;
     load_hr();   // next iteration's Hr columns (the factor in c0/c1 is dead now)
     wave_sync();
+    if constexpr (D::WH) {
+      // the wheel rows' residual at the new iterate moves the multiplier centre (a converged env's
+      // iterate no longer moves: its centre stays)
+      const double r = aw_rows(sVy);
+      cw = done ? cw : fma(dw, r, cw);
+      aw_cols(cw, wnu0, wnu1);
+      rwmax = row_max(fabs(r));
+    }
     STAMP_END(7);
   }
 #ifdef OSC_STAMPS
@@ -1741,6 +1905,17 @@ __device__ __forceinline__ void ipm_block(
   // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
   // discarded.
   bool refined = false;
+  // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
+  // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
+  // every other multiplier from the design vector itself.
+  auto put_wheel_duals = [&](double nu) {
+    if constexpr (D::WH) {
+      if (want_dual && write_out && l < NW)
+        const_cast<double*>(ws)[static_cast<size_t>(env) * D::WS + D::W_NU + l] = nu;
+    }
+  };
+  // the duals ask the refinement for more steps (its multipliers converge more slowly than y)
+  const int refine_steps = P->refine_steps + ((D::WH && want_dual) ? P->refine_dual_extra : 0);
   if constexpr (RF != kRfNone) {
     const bool mine = valid && st == OSC_SOLVE_OK;
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
@@ -1756,6 +1931,8 @@ __device__ __forceinline__ void ipm_block(
       const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg;
       double ya0 = y0, ya1 = y1;
       bool viol_env = false;
+      // wheel rows: always active, penalty D_w (already in K_A through Hr), multipliers nur
+      double nur = cw;
       const double* wenv = ws + static_cast<size_t>(env) * D::WS;
       const double* rX = kRefG ? wenv + D::W_X : sRX;
       const double* rH = kRefG ? wenv + D::W_HD : sRH;
@@ -1785,6 +1962,7 @@ __device__ __forceinline__ void ipm_block(
         for (int t = 0; t < NRL; ++t) sDr[l + kRow * t] = Dr[t];
         ya0 = y0;
         ya1 = y1;
+        nur = cw;
         sVy[j0] = y0;
         if (v1) sVy[j1] = y1;
         wave_sync();
@@ -1830,6 +2008,9 @@ __device__ __forceinline__ void ipm_block(
           static_assert(D::NV * D::NY1P <= even(NY * NY) && D::W_X % 2 == 0 &&
                         NT * kWave * 2 <= even(NY * NY), "X (whole DMA rows) in Hr's region");
           if (round == 0) {
+            // the loop's last Hr column reads of this region (load_hr) have returned before the DMA
+            // overwrites it (K_A's assembly consumed only some of them)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             static_for<0, kEnvPerWave>([&](auto G) {
               constexpr int g = decltype(G)::value;
               const int eg = blk * kEnvPerWave + g < nenv ? blk * kEnvPerWave + g : nenv - 1;
@@ -1879,7 +2060,7 @@ __device__ __forceinline__ void ipm_block(
         wave_sync();
         STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
-        for (int k = 0; k < P->refine_steps; ++k) {
+        for (int k = 0; k < refine_steps; ++k) {
           // dv = X [y; 1] (rows l, l + 16) -> sXb
 #pragma unroll
           for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
@@ -1887,7 +2068,7 @@ __device__ __forceinline__ void ipm_block(
             if (rr < NV) {
               const double* xr = rX + rr * NY1P;
               double a = xr[NY];
-#pragma unroll(kUr)
+#pragma unroll kUr
               for (int i = 0; i < NY; ++i) a = fma(xr[i], sVy[i], a);
               sXb[rr] = a;
             }
@@ -1902,7 +2083,7 @@ __device__ __forceinline__ void ipm_block(
             if (rr < NV) {
               const double* hr = rH + rr * NV;
               double a = rG[rr];
-#pragma unroll(kUr)
+#pragma unroll kUr
               for (int i = 0; i < NV; ++i) a = fma(hr[i], sXb[i], a);
               gxr[t] = a;
             }
@@ -1916,7 +2097,7 @@ __device__ __forceinline__ void ipm_block(
           wave_sync();
           // r_j = X[:, j]' gx + diag_j y_j + (G_A' mu)_j for the lane's two variables
           double r0 = (j0 < NU ? wu : wz) * ya0, r1 = (jj1 < NU ? wu : wz) * ya1;
-#pragma unroll(kUr)
+#pragma unroll kUr
           for (int i = 0; i < NV; ++i) {
             r0 = fma(rX[i * NY1P + j0], sDr[i], r0);
             r1 = fma(rX[i * NY1P + jj1], sDr[i], r1);
@@ -1925,6 +2106,14 @@ __device__ __forceinline__ void ipm_block(
           GTw2(sVr, gm0, gm1);
           r0 += gm0;
           r1 += gm1;
+          double rw = 0.0;   // WH: the wheel rows' residual A~ [y; 1] (lane w)
+          if constexpr (D::WH) {
+            double q0, q1;
+            aw_cols(nur, q0, q1);   // + A~' nu
+            r0 += q0;
+            r1 += q1;
+            rw = aw_rows(sVy);
+          }
           wave_sync();
           double R3[NRL];
 #pragma unroll
@@ -1935,6 +2124,12 @@ __device__ __forceinline__ void ipm_block(
           wave_sync();
           double b0, b1;
           GTw2(sVr, b0, b1);
+          if constexpr (D::WH) {   // + D_w A~' A~ [y; 1]
+            double e0, e1;
+            aw_cols(dw * rw, e0, e1);
+            b0 += e0;
+            b1 += e1;
+          }
           double d0 = -r0 - b0, d1 = -r1 - b1;
           ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, d0, d1, l);
           sVy2[j0] = d0;
@@ -1948,6 +2143,7 @@ __device__ __forceinline__ void ipm_block(
           sVy[j0] = ya0;
           if (v1) sVy[j1] = ya1;
           wave_sync();
+          if constexpr (D::WH) nur = fma(dw, aw_rows(sVy), nur);   // nu += D_w A~ [y + dy; 1]
         }
         // rows the refined point violates join the active set
         double nviol = 0.0;
@@ -1964,13 +2160,20 @@ __device__ __forceinline__ void ipm_block(
       // keep the refined iterate when it is feasible, finite and close to the interior point's
       const double mv = fmax(fabs(ya0 - y0), v1 ? fabs(ya1 - y1) : 0.0);
       const double my = fmax(fabs(y0), v1 ? fabs(y1) : 0.0);
-      const double ok = (isfinite(ya0) && isfinite(ya1) && mv <= 1e-3 * (1.0 + my)) ? 1.0 : 0.0;
-      const bool keep = !viol_env && row_min(ok) == 1.0;
+      const double ok =
+          (isfinite(ya0) && isfinite(ya1) && mv <= P->refine_max_move * (1.0 + my)) ? 1.0 : 0.0;
+      // (WH: and the wheel rows hold at the refined point; sVy holds it)
+      const double wres = D::WH ? row_max(fabs(aw_rows(sVy))) : 0.0;
+      const bool keep = !viol_env && row_min(ok) == 1.0 && wres <= ytol;
       if (mine && keep) {
         y0 = ya0;
         y1 = ya1;
         refined = true;
       }
+      // a converged env whose refinement is rejected keeps the interior point's iterate, and says
+      // so: it is only as accurate as the interior point's stop
+      if (mine && !keep) st = OSC_SOLVE_UNREFINED;
+      put_wheel_duals((mine && keep) ? nur : cw);
       wave_sync();
       sVy[j0] = y0;
       if (v1) sVy[j1] = y1;
@@ -1981,8 +2184,12 @@ __device__ __forceinline__ void ipm_block(
 #ifdef OSC_STAMPS
   if constexpr (RF == kRfFused) STAMP_STORE();
 #endif
+  if (!refined) put_wheel_duals(cw);
   // ---------------- outputs: tau = y_u;  x = (dv, u, z) with dv = X [y; 1] -----------------
-  if (REFINE && !refined) write_out = false;   // the interior point kernel's outputs stand
+  if (REFINE && !refined) {   // the interior point kernel's outputs stand
+    if (write_out && l == 0 && gstatus && st == OSC_SOLVE_UNREFINED) gstatus[env] = st;
+    write_out = false;
+  }
   if (l < NU) {
     const double tq = sVy[l];
     sTau[l] = tq;
@@ -2039,12 +2246,12 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
-    int fixup) {
+    int flags) {
   // one-wave variant: four workgroups per CU (160 KB of LDS), never five
   static_assert(!SMALL || ipm_lds_doubles<D, SMALL, RF>() * 8 <= 160 * 1024 / 4, "IPM LDS");
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, RF>()];
   ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
-                                    gstatus, giters, gwarm, fixup, sm);
+                                    gstatus, giters, gwarm, flags, sm);
 }
 
 // The full-space refinement pass (torque coordinates): the same body with the interior-point
@@ -2053,10 +2260,11 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
 template <class D, bool SMALL>
 __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_refine_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
-    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx) {
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
+    int32_t* __restrict__ gstatus) {
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, kRfOnly>()];
   ipm_block<D, SMALL, false, kRfOnly>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
-                                   nullptr, nullptr, nullptr, 0, sm);
+                                   gstatus, nullptr, nullptr, 0, sm);
 }
 
 // Two models' interior point in one grid, one wavefront per SIMD (the one-wave variant of both):
@@ -2078,15 +2286,219 @@ __global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, Pair
                                        B.status, B.iters, nullptr, 0, sm);
 }
 
+// ============================ kernel 3: dual solution (optional output) ======================
+// The reference's OsqpSolver::dual_solution (operational_space_controller.h:534-535) over its rows
+// A = [Aeq; Aineq; I_n] (osc.h:483-497; with wheel rows Aeq = [dynamics; wheel rows]) in OSQP's
+// sign convention (H x + f + A'y = 0, y >= 0 on an active upper bound, <= 0 on a lower one),
+// recovered from the returned design vector x = (dv, u, z) by stationarity:
+//   dynamics rows  nu = -M^-1 (H_dv dv + f_dv + E'nu_w)             (the dv block)
+//   wheel rows     nu_w: the refinement's multipliers (W_NU), unscaled s_w nu~_w
+//   u box rows     nu_a - 2 (w_tau + w_reg) u                        (the u block)
+//   contact k      r_k = 2 w_reg z_k - Jc_k'nu must be balanced by its active rows: the pyramid
+//                  rows, fz >= 0, fz <= big_number (a tiny non-negative least squares over the
+//                  active rows, every subset of at most three -- Caratheodory -- tried: the apex,
+//                  where five rows are active on three forces, has non-unique multipliers);
+//                  fx, fy have no bounds (y = 0); a contact off the ground (l = u = 0) takes -r_k.
+// A design vector that is not optimal shows up as a residual of the z block, a u-box multiplier of
+// the wrong sign or one on an inactive bound -- the KKT certificate of tests/test_gpu_wheels.py.
+// One 64-lane wavefront per env; M is factored in LDS (left-looking Cholesky, lane = row).
+template <class D>
+__global__ __launch_bounds__(kWave) void osc_dual_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
+    const double* __restrict__ gJ, const double* __restrict__ gmask,
+    const double* __restrict__ gwd, const double* __restrict__ ws, const double* __restrict__ gx,
+    double* __restrict__ gy) {
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NW = D::NW, NX = D::NX,
+                S = D::S, NB = D::NB;
+  constexpr int NROW = NV + NW + 4 * NC + NX, JC0 = 3 * (NS - NC);
+  static_assert(NC <= kWave, "one lane per contact");
+  __shared__ double sL[NV * NV];
+  __shared__ double sg[NV];
+  __shared__ double snu[NW > 0 ? NW : 1];
+  __shared__ double sq[NC * 6];   // per contact: 4 pyramid rows, fz >= 0, fz <= ub (>= 0 each)
+  __shared__ double sr[NC * 3];   // per contact: r_k
+  const int env = static_cast<int>(blockIdx.x), lane = static_cast<int>(threadIdx.x);
+  if (env >= nenv) return;
+  const double* w = ws + static_cast<size_t>(env) * D::WS;
+  const double* x = gx + static_cast<size_t>(env) * NX;
+  const double* J = gJ + static_cast<size_t>(env) * S * NV;
+  const double* mask = gmask + static_cast<size_t>(env) * NC;
+  for (int p = lane; p < NV * NV; p += kWave) sL[p] = gM[static_cast<size_t>(env) * NV * NV + p];
+  if (lane < NW) snu[lane] = w[D::W_DW + 2 + lane] * w[D::W_NU + lane];
+  __syncthreads();
+  if (lane < NV) {   // g_x = H_dv dv + f_dv (+ E' nu_w)
+    double a = w[D::W_GD + lane];
+    for (int j = 0; j < NV; ++j) a = fma(w[D::W_HD + lane * NV + j], x[j], a);
+    if constexpr (D::WH) {
+      const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
+      for (int i = 0; i < NC; ++i) {
+        double er = 0.0, el = 0.0;
+        for (int c = 0; c < 3; ++c) {
+          const double jv = J[(JC0 + 3 * i + c) * NV + lane];
+          er = fma(wd[6 * i + c], jv, er);
+          el = fma(wd[6 * i + 3 + c], jv, el);
+        }
+        if (lane == P->wheel_dof[i]) er -= P->wheel_radius[i];
+        a = fma(mask[i] * er, snu[2 * i], a);
+        a = fma(mask[i] * el, snu[2 * i + 1], a);
+      }
+    }
+    sg[lane] = -a;
+  }
+  __syncthreads();
+  for (int k = 0; k < NV; ++k) {   // M = L L' (lower triangle of sL), column k
+    double t = 0.0;
+    if (lane >= k && lane < NV) {
+      t = sL[lane * NV + k];
+      for (int p = 0; p < k; ++p) t = fma(-sL[lane * NV + p], sL[k * NV + p], t);
+      sL[lane * NV + k] = t;
+    }
+    __syncthreads();
+    const double dk = sqrt(sL[k * NV + k]);
+    __syncthreads();
+    if (lane >= k && lane < NV) sL[lane * NV + k] = (lane == k) ? dk : t / dk;
+    __syncthreads();
+  }
+  if (lane == 0) {   // L L' nu = -g_x
+    for (int i = 0; i < NV; ++i) {
+      double a = sg[i];
+      for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], sg[p], a);
+      sg[i] = a / sL[i * NV + i];
+    }
+    for (int i = NV - 1; i >= 0; --i) {
+      double a = sg[i];
+      for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], sg[p], a);
+      sg[i] = a / sL[i * NV + i];
+    }
+  }
+  __syncthreads();
+  if (lane < NC) {   // contact `lane`: r_k, then its rows' multipliers
+    const int k = lane;
+    const double wz = 2.0 * P->w_reg, mu = P->mu;
+    double r[3], f[3];
+    for (int c = 0; c < 3; ++c) {
+      f[c] = x[NV + NU + 3 * k + c];
+      double a = wz * f[c];
+      for (int i = 0; i < NV; ++i) a = fma(-J[(JC0 + 3 * k + c) * NV + i], sg[i], a);
+      r[c] = a;
+      sr[3 * k + c] = a;
+    }
+    double q[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (mask[k] != 0.0) {
+      // rows g_i' f <= h_i: pyramid (sx, sy, -mu) <= 0, -fz <= -lb, fz <= ub
+      const double ub = P->z_ub[2] * mask[k], lb = P->z_lb[2] * mask[k];
+      double g[6][3], h[6];
+      for (int i = 0; i < 4; ++i) {
+        g[i][0] = (i & 1) ? -1.0 : 1.0;
+        g[i][1] = (i >= 2) ? -1.0 : 1.0;
+        g[i][2] = -mu;
+        h[i] = 0.0;
+      }
+      g[4][0] = g[4][1] = 0.0; g[4][2] = -1.0; h[4] = -lb;
+      g[5][0] = g[5][1] = 0.0; g[5][2] = 1.0;  h[5] = ub;
+      const double tol = 1e-8 * (1.0 + fmax(fabs(f[0]), fmax(fabs(f[1]), fabs(f[2]))));
+      int act = 0;
+      for (int i = 0; i < 6; ++i) {
+        const double gi = g[i][0] * f[0] + g[i][1] * f[1] + g[i][2] * f[2] - h[i];
+        const bool finite = (i < 4) || fabs(h[i]) < P->inf_thresh;
+        if (finite && gi >= -tol) act |= 1 << i;
+      }
+      // min |r + G_S' m| over m >= 0, S a subset of the active rows with |S| <= 3
+      double best = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+      int bestS = 0;
+      double bm[3] = {0.0, 0.0, 0.0};
+      for (int S = 1; S < 64; ++S) {
+        if ((S & act) != S || __builtin_popcount(S) > 3) continue;
+        int id[3], n = 0;
+        for (int i = 0; i < 6; ++i)
+          if (S >> i & 1) id[n++] = i;
+        double A[3][3], bb[3];   // (G_S G_S') m = -G_S r
+        for (int a = 0; a < n; ++a) {
+          bb[a] = -(g[id[a]][0] * r[0] + g[id[a]][1] * r[1] + g[id[a]][2] * r[2]);
+          for (int c = 0; c < n; ++c)
+            A[a][c] = g[id[a]][0] * g[id[c]][0] + g[id[a]][1] * g[id[c]][1] + g[id[a]][2] * g[id[c]][2];
+        }
+        bool ok = true;   // Gaussian elimination with partial pivoting, n <= 3
+        for (int c = 0; c < n && ok; ++c) {
+          int p = c;
+          for (int a = c + 1; a < n; ++a)
+            if (fabs(A[a][c]) > fabs(A[p][c])) p = a;
+          if (fabs(A[p][c]) < 1e-12) { ok = false; break; }
+          if (p != c) {
+            for (int e = 0; e < n; ++e) { const double t = A[c][e]; A[c][e] = A[p][e]; A[p][e] = t; }
+            const double t = bb[c]; bb[c] = bb[p]; bb[p] = t;
+          }
+          for (int a = c + 1; a < n; ++a) {
+            const double fct = A[a][c] / A[c][c];
+            for (int e = c; e < n; ++e) A[a][e] -= fct * A[c][e];
+            bb[a] -= fct * bb[c];
+          }
+        }
+        if (!ok) continue;
+        double m[3];
+        for (int a = n - 1; a >= 0; --a) {
+          double t = bb[a];
+          for (int e = a + 1; e < n; ++e) t -= A[a][e] * m[e];
+          m[a] = t / A[a][a];
+        }
+        bool nonneg = true;
+        for (int a = 0; a < n; ++a) nonneg = nonneg && m[a] >= 0.0;
+        if (!nonneg) continue;
+        double res = 0.0;
+        for (int c = 0; c < 3; ++c) {
+          double t = r[c];
+          for (int a = 0; a < n; ++a) t += m[a] * g[id[a]][c];
+          res += t * t;
+        }
+        if (res < best * (1.0 - 1e-12)) {
+          best = res;
+          bestS = S;
+          for (int a = 0; a < 3; ++a) bm[a] = a < n ? m[a] : 0.0;
+        }
+      }
+      for (int i = 0, a = 0; i < 6; ++i)
+        if (bestS >> i & 1) q[i] = bm[a++];
+    }
+    for (int i = 0; i < 6; ++i) sq[6 * k + i] = q[i];
+  }
+  __syncthreads();
+  double* y = gy + static_cast<size_t>(env) * NROW;
+  const double wu = 2.0 * (P->w_torque + P->w_reg);
+  for (int r = lane; r < NROW; r += kWave) {
+    double v = 0.0;
+    if (r < NV) {
+      v = sg[r];
+    } else if (r < NV + NW) {
+      v = snu[r - NV];
+    } else if (r < NV + NW + 4 * NC) {
+      const int k = (r - NV - NW) / 4, rr = (r - NV - NW) % 4;
+      v = sq[6 * k + rr];
+    } else {
+      const int c = r - NV - NW - 4 * NC;   // design variable of the box row
+      if (c >= NV && c < NV + NU) {
+        v = sg[NB + c - NV] - wu * x[c];
+      } else if (c >= NV + NU) {
+        const int zc = c - NV - NU, k = zc / 3;
+        if (mask[k] == 0.0) v = -sr[zc];
+        else if (zc % 3 == 2) v = sq[6 * k + 5] - sq[6 * k + 4];
+      }
+    }
+    y[r] = v;
+  }
+}
+
 using Go2 = Dims<18, 12, 4, 5>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites
 using Walter = Dims<14, 8, 8, 17>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
+using WalterW = Dims<14, 8, 8, 17, true>;   // + the wheel no-slip rows (opt-in)
 
-enum KernelId { K_NONE = 0, K_GO2 = 1, K_WALTER = 2 };
+enum KernelId { K_NONE = 0, K_GO2 = 1, K_WALTER = 2, K_WALTER_WHEELS = 3 };
 
 KernelId select_kernel(const osc_model_desc& d) {
-  if (d.nv == Go2::NV && d.nu == Go2::NU && d.nc == Go2::NC && d.ns == Go2::NS) return K_GO2;
+  const bool wheels = d.wheel_rows != 0;
+  if (d.nv == Go2::NV && d.nu == Go2::NU && d.nc == Go2::NC && d.ns == Go2::NS)
+    return wheels ? K_NONE : K_GO2;
   if (d.nv == Walter::NV && d.nu == Walter::NU && d.nc == Walter::NC && d.ns == Walter::NS)
-    return K_WALTER;
+    return wheels ? K_WALTER_WHEELS : K_WALTER;
   return K_NONE;
 }
 
@@ -2094,7 +2506,7 @@ int ww_doubles(KernelId k) {
   switch (k) {
     case K_GO2: return Go2::WW;
     case K_WALTER: return Walter::WW;
-    default: return 0;
+    default: return 0;   // (no warm start with wheel rows)
   }
 }
 
@@ -2102,6 +2514,16 @@ int ws_doubles(KernelId k) {
   switch (k) {
     case K_GO2: return Go2::WS;
     case K_WALTER: return Walter::WS;
+    case K_WALTER_WHEELS: return WalterW::WS;
+    default: return 0;
+  }
+}
+
+int dual_rows(KernelId k) {
+  switch (k) {
+    case K_GO2: return Go2::NV + 4 * Go2::NC + Go2::NX;
+    case K_WALTER: return Walter::NV + 4 * Walter::NC + Walter::NX;
+    case K_WALTER_WHEELS: return WalterW::NV + WalterW::NW + 4 * WalterW::NC + WalterW::NX;
     default: return 0;
   }
 }
@@ -2132,6 +2554,10 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
       return OSC_ERR_INVALID_ARGUMENT;
   for (int i = 0; i < d.nu; ++i)
     if (!(d.u_lb[i] <= d.u_ub[i])) return OSC_ERR_INVALID_ARGUMENT;
+  if (d.wheel_rows != 0 && d.wheel_rows != 1) return OSC_ERR_INVALID_ARGUMENT;
+  for (int i = 0; d.wheel_rows && i < d.nc; ++i)
+    if (d.wheel_dof[i] < -1 || d.wheel_dof[i] >= d.nv || !std::isfinite(d.wheel_radius[i]))
+      return OSC_ERR_INVALID_ARGUMENT;
   const KernelId kid = select_kernel(d);
   if (kid == K_NONE) return OSC_ERR_UNSUPPORTED_DIMS;
 
@@ -2177,6 +2603,25 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
   if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);
   if (const char* e = std::getenv("OSC_WARM_CENTER")) hp.warm_center = std::atof(e);
+  // a refinement that moves y by more than this (relative) is rejected (OSC_SOLVE_UNREFINED);
+  // the variable exists so a test can force rejections
+  hp.refine_max_move = 1e-3;
+  hp.refine_dual_extra = 4;
+  if (const char* e = std::getenv("OSC_REFINE_MAX_MOVE")) hp.refine_max_move = std::atof(e);
+  // The YAML's Go2 stop (eps_mu 1e-9) presumes the refinement finishes the solve; without it the
+  // interior point runs to 1e-12 itself.
+  if (hp.refine_steps <= 0) hp.eps_mu = std::fmin(hp.eps_mu, 1e-12);
+  // wheel no-slip rows: penalty D_w = 1e3 x max diag(Hr) on the unit-norm rows,
+  // interior point stops once every row holds to 1e-8 (the refinement then solves them exactly)
+  for (int i = 0; i < OSC_MAX_SITES; ++i) hp.wheel_dof[i] = -1;
+  for (int i = 0; d.wheel_rows && i < d.nc; ++i) {
+    hp.wheel_dof[i] = d.wheel_dof[i];
+    hp.wheel_radius[i] = d.wheel_radius[i];
+  }
+  hp.wheel_penalty = 1e3;
+  hp.wheel_tol = 1e-8;
+  if (const char* e = std::getenv("OSC_WHEEL_PENALTY")) hp.wheel_penalty = std::atof(e);
+  if (const char* e = std::getenv("OSC_WHEEL_TOL")) hp.wheel_tol = std::atof(e);
 
   osc_model* m = new (std::nothrow) osc_model;
   if (!m) return OSC_ERR_DEVICE;
@@ -2192,8 +2637,9 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   // two-waves variant, except for the 32-column WaLTER system, whose Newton matrix does not fit
   // two waves' register budget (scratch spills): it always runs one wave per SIMD with AGPR
   // spill space (MI355X, 32,768 envs: 2.61 vs 2.95 ms; tools/variant_sweep.sh).
-  m->small_batch_max = (kid == K_WALTER) ? INT32_MAX : kEnvPerWave * 4 * cus;
+  m->small_batch_max = (kid == K_GO2) ? kEnvPerWave * 4 * cus : INT32_MAX;
   if (const char* e = std::getenv("OSC_SMALL_BATCH_MAX")) m->small_batch_max = std::atoi(e);
+  if (kid == K_WALTER_WHEELS) m->small_batch_max = INT32_MAX;   // (one-wave kernel only)
   if (hipMalloc(&m->dparams, sizeof(DevParams)) != hipSuccess ||
       hipMemcpy(m->dparams, &hp, sizeof(DevParams), hipMemcpyHostToDevice) != hipSuccess) {
     if (m->dparams) (void)hipFree(m->dparams);
@@ -2241,17 +2687,23 @@ template <class D>
 void launch_t(const osc_model* model, int32_t nenv, const double* M, const double* C,
               const double* J, const double* b, const double* T, const double* mask, double* tau,
               double* x, int32_t* status, int32_t* iters, double* ws, double* warm, hipStream_t s,
-              unsigned stages) {
+              unsigned stages, const double* wdir, double* y) {
   if (stages & kAssemble) {
     // one env per 64-lane wavefront (four envs per wavefront measured no faster: Go2 4,096
     // 35.3 vs 33.7 us)
     hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
-                       model->dparams, nenv, M, C, J, b, T, mask, ws);
+                       model->dparams, nenv, M, C, J, b, T, mask, ws, wdir);
   }
-  if (stages & kInteriorPoint) {
-    // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one
-    // wave per SIMD, Hr in LDS where it fits); otherwise the two-waves-per-SIMD variant.
-    const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
+  if (!(stages & kInteriorPoint)) return;
+  // All wavefronts resident at once (<= one per SIMD): the latency-optimised variant (one wave
+  // per SIMD, Hr in LDS where it fits); otherwise the two-waves-per-SIMD variant.
+  const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
+  const int flags = y != nullptr ? 2 : 0;   // hand the multipliers to the dual kernel
+  if constexpr (D::WH) {
+    // wheel rows: the cold one-wave solve with the refinement fused (launch() checked the rest)
+    hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                       model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
+  } else {
     // A warm-started solve is followed by a cold fix-up pass over the wavefronts that hold an
     // env the warm start did not bring to convergence (it needs the per-env status: the
     // caller's array, else scratch at the end of the workspace).
@@ -2259,23 +2711,23 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
       status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
     const bool small = nenv <= model->small_batch_max;
     // Every cold solve runs the refinement in the same wavefront (kRfFused), and so does the
-    // one-wave warm solve; warm past one wave per SIMD the fused two-wave kernel spills (Go2 65,536
-    // warm 50.0 -> 44.5 M solves/s), so that case keeps the separate refinement pass.
+    // one-wave warm solve; warm past one wave per SIMD the fused two-wave kernel spills (Go2
+    // 65,536 warm 50.0 -> 44.5 M solves/s), so that case keeps the separate refinement pass.
     const bool fused = warm == nullptr && model->refine;
     const bool fused_warm = small && warm != nullptr && model->refine;
     if (warm == nullptr) {
       if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
       else if (fused)
         hipLaunchKernelGGL((osc_ipm_kernel<D, false, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
       else if (small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
       else
         hipLaunchKernelGGL((osc_ipm_kernel<D, false, false>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, 0);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
     } else if (fused_warm) {
       // warm-started: the refinement runs in the same wavefront too, in pass 0 for the envs the
       // warm start converged and in the cold fix-up pass for the ones it redoes
@@ -2295,24 +2747,40 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     }
     if (model->refine && !fused && !fused_warm)   // (warm, past one wave per SIMD)
       hipLaunchKernelGGL((osc_refine_kernel<D, false>), dim3(nb), dim3(kWave), 0, s,
-                         model->dparams, nenv, mask, ws, tau, x);
+                         model->dparams, nenv, mask, ws, tau, x, status);
   }
+  if (y != nullptr)
+    hipLaunchKernelGGL(osc_dual_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
+                       model->dparams, nenv, M, J, mask, wdir, ws, x, y);
 }
 
 bool misaligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
 
+// A model's kernels read its parameters from the device it was created on: launches go there.
+bool on_model_device(const osc_model* model) {
+  int cur = -1;
+  return hipGetDevice(&cur) == hipSuccess && cur == model->device;
+}
+
 int launch(const osc_model* model, int32_t nenv, const double* M, const double* C, const double* J,
            const double* b, const double* T, const double* contact_mask, double* tau, double* x,
            int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes,
-           void* stream, unsigned stages, double* warm = nullptr) {
+           void* stream, unsigned stages, double* warm = nullptr, const double* wdir = nullptr,
+           double* y = nullptr) {
   if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
   if (nenv == 0) return OSC_OK;
+  if (!on_model_device(model)) return OSC_ERR_INVALID_ARGUMENT;
   if (!contact_mask || misaligned16(contact_mask)) return OSC_ERR_INVALID_ARGUMENT;
   if ((stages & kAssemble) && (!M || !C || !J || !b || !T || misaligned16(M) ||
                                misaligned16(C) || misaligned16(J) || misaligned16(b) ||
                                misaligned16(T)))
     return OSC_ERR_INVALID_ARGUMENT;   // 16-byte alignment: vectorised staging loads
   if ((stages & kInteriorPoint) && !tau) return OSC_ERR_INVALID_ARGUMENT;
+  const bool wheels = model->kid == K_WALTER_WHEELS;
+  if (wheels && warm != nullptr) return OSC_ERR_UNSUPPORTED_DIMS;   // no warm start with them
+  if (wheels && (stages & kAssemble) && wdir == nullptr) return OSC_ERR_INVALID_ARGUMENT;
+  if (y != nullptr && (x == nullptr || (stages & kBoth) != kBoth)) return OSC_ERR_INVALID_ARGUMENT;
+  if (y != nullptr && !model->refine) return OSC_ERR_INVALID_ARGUMENT;   // (fused path only)
   // A split call hands the reduced QP over in the caller's workspace; only the fused call may
   // take scratch of its own.
   if (stages != kBoth && !workspace) return OSC_ERR_INVALID_ARGUMENT;
@@ -2332,11 +2800,15 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
   switch (model->kid) {
     case K_GO2:
       launch_t<Go2>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, warm, s,
-                    stages);
+                    stages, nullptr, y);
       break;
     case K_WALTER:
       launch_t<Walter>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, warm, s,
-                       stages);
+                       stages, nullptr, y);
+      break;
+    case K_WALTER_WHEELS:
+      launch_t<WalterW>(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, ws, warm,
+                        s, stages, wdir, y);
       break;
     default:
       rc = OSC_ERR_UNSUPPORTED_DIMS;
@@ -2355,6 +2827,33 @@ extern "C" int osc_batch_solve(const osc_model* model, int32_t nenv, const doubl
                                size_t workspace_bytes, void* stream) {
   return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
                 workspace_bytes, stream, kBoth);
+}
+
+extern "C" int osc_dual_rows(const osc_model* model, int32_t* rows) {
+  if (!model || !rows) return OSC_ERR_INVALID_ARGUMENT;
+  *rows = dual_rows(model->kid);
+  return OSC_OK;
+}
+
+extern "C" int osc_batch_solve_ex(const osc_model* model, int32_t nenv, const double* M,
+                                  const double* C, const double* J, const double* b,
+                                  const double* T, const double* contact_mask,
+                                  const osc_solve_extras* extras, double* tau, double* x,
+                                  int32_t* status, int32_t* iters, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  const double* wdir = extras ? extras->wheel_dir : nullptr;
+  if (wdir && misaligned16(wdir)) return OSC_ERR_INVALID_ARGUMENT;
+  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
+                workspace_bytes, stream, kBoth, nullptr, wdir, extras ? extras->y : nullptr);
+}
+
+extern "C" int osc_batch_assemble_ex(const osc_model* model, int32_t nenv, const double* M,
+                                     const double* C, const double* J, const double* b,
+                                     const double* T, const double* contact_mask,
+                                     const double* wheel_dir, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  return launch(model, nenv, M, C, J, b, T, contact_mask, nullptr, nullptr, nullptr, nullptr,
+                workspace, workspace_bytes, stream, kAssemble, nullptr, wheel_dir);
 }
 
 extern "C" int osc_batch_assemble(const osc_model* model, int32_t nenv, const double* M,
@@ -2405,7 +2904,8 @@ extern "C" int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, v
         !j.M || !j.C || !j.J || !j.b || !j.T || misaligned16(j.M) || misaligned16(j.C) ||
         misaligned16(j.J) || misaligned16(j.b) || misaligned16(j.T))
       return OSC_ERR_INVALID_ARGUMENT;
-    if (j.model->kid == K_NONE) return OSC_ERR_UNSUPPORTED_DIMS;
+    if (j.model->kid == K_NONE || j.model->kid == K_WALTER_WHEELS) return OSC_ERR_UNSUPPORTED_DIMS;
+    if (!on_model_device(j.model)) return OSC_ERR_INVALID_ARGUMENT;   // one device per call
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (njobs == 2 && jobs[0].nenv > 0 && jobs[1].nenv > 0 && jobs[0].model->kid != jobs[1].model->kid &&

@@ -220,6 +220,34 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   // WaLTER at 1e-12 (at 1e-9 its degenerate contact rows are not yet resolved; numpy model)
   desc->eps_mu = std::strcmp(robot, "unitree_go2") == 0 ? 1e-9 : 1e-12;
   desc->max_iter = 50;   // normal solves take <= 24; the margin covers a re-centred stall
+  // optional wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240, commented out
+  // upstream): `wheel_no_slip: true`, `wheel_radius: r` (or one per wheel, the design's 0.065 at
+  // :64), `wheel_dofs: [k_0, ...]` (the dof of each wheel's joint, the design's jnt_dofadr lookup
+  // at :64-94; -1 = none).  Absent keys: off, the reference's QP.
+  const std::string& ns_flag = y.scalars["wheel_no_slip"];
+  if (ns_flag == "true" || ns_flag == "True" || ns_flag == "1") {
+    desc->wheel_rows = 1;
+    const auto& rl = y.lists["wheel_radius"];
+    double r = 0.0;
+    const bool scalar_r = rl.empty() && to_double(y.scalars["wheel_radius"], &r);
+    const auto& dl = y.lists["wheel_dofs"];
+    if ((!scalar_r && static_cast<int>(rl.size()) != info->nc) ||
+        static_cast<int>(dl.size()) != info->nc) {
+      std::fprintf(stderr, "osc_desc_from_yaml: %s: wheel_radius / wheel_dofs need %d entries\n",
+                   path.c_str(), info->nc);
+      return OSC_ERR_IO;
+    }
+    for (int i = 0; i < info->nc; ++i) {
+      double k = 0.0;
+      if (!scalar_r && !to_double(rl[i], &r)) return OSC_ERR_IO;
+      if (!to_double(dl[i], &k) || k != static_cast<int>(k) || k < -1 || k >= info->nv)
+        return OSC_ERR_IO;
+      desc->wheel_radius[i] = r;
+      desc->wheel_dof[i] = static_cast<int32_t>(k);
+    }
+  } else if (!ns_flag.empty() && ns_flag != "false" && ns_flag != "False" && ns_flag != "0") {
+    return OSC_ERR_IO;
+  }
   return OSC_OK;
 }
 

@@ -17,7 +17,7 @@ OSC_MAX_NU = 16
 
 STATUS_NAMES = {0: "OSC_OK", 1: "OSC_ERR_INVALID_ARGUMENT", 2: "OSC_ERR_UNSUPPORTED_DIMS",
                 3: "OSC_ERR_IO", 4: "OSC_ERR_DEVICE", 5: "OSC_ERR_NO_DEVICE"}
-SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL = 0, 1, 2
+SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL, SOLVE_UNREFINED = 0, 1, 2, 3
 
 EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
                     "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_batch_solve_qpos_warm", "osc_batch_solve_multi",
                     "osc_kin_desc_from_mjcf", "osc_kin_desc_from_mjcf_robot",
                     "osc_contact_geom_table", "osc_tumbling_params_default",
-                    "osc_tumbling_targets")
+                    "osc_tumbling_targets", "osc_dual_rows", "osc_batch_solve_ex",
+                    "osc_batch_assemble_ex")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -53,7 +54,15 @@ class OscModelDesc(ctypes.Structure):
         ("infinity", ctypes.c_double),
         ("eps_mu", ctypes.c_double),
         ("max_iter", ctypes.c_int32),
+        ("wheel_rows", ctypes.c_int32),
+        ("wheel_dof", ctypes.c_int32 * OSC_MAX_SITES),
+        ("wheel_radius", ctypes.c_double * OSC_MAX_SITES),
     ]
+
+
+class OscSolveExtras(ctypes.Structure):
+    """osc_solve_extras (include/osc_batch.h): per-call extras of osc_batch_solve_ex."""
+    _fields_ = [("wheel_dir", ctypes.c_void_p), ("y", ctypes.c_void_p)]
 
 
 class OscTumblingParams(ctypes.Structure):
@@ -152,6 +161,13 @@ def lib() -> ctypes.CDLL:
     L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 6 + [ctypes.c_size_t, vp,
                                                                          ctypes.c_size_t, vp]
     L.osc_batch_solve_assembled_warm.restype = ctypes.c_int
+    L.osc_dual_rows.argtypes = [vp, ctypes.POINTER(i32)]
+    L.osc_dual_rows.restype = ctypes.c_int
+    L.osc_batch_solve_ex.argtypes = [vp, i32] + [vp] * 6 + [ctypes.POINTER(OscSolveExtras)] + \
+        [vp] * 4 + [vp, ctypes.c_size_t, vp]
+    L.osc_batch_solve_ex.restype = ctypes.c_int
+    L.osc_batch_assemble_ex.argtypes = [vp, i32] + [vp] * 7 + [vp, ctypes.c_size_t, vp]
+    L.osc_batch_assemble_ex.restype = ctypes.c_int
     L.osc_batch_solve_multi.argtypes = [ctypes.POINTER(OscBatchJob), i32, vp]
     L.osc_batch_solve_multi.restype = ctypes.c_int
     kp = ctypes.POINTER(OscKinDesc)

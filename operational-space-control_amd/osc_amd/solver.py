@@ -6,6 +6,9 @@ Reference interface this mirrors (paths relative to the reference's operational-
   * update_optimization_data() + update_optimization() + solve_optimization()  osc.h:457-536
       -> OSCBatchSolver.solve(M, C, J, b, T, mask)          (all environments in one launch)
   * get_torque_command() -> tau;  get_solution() -> x        osc.h:230-238
+  * OsqpSolver::dual_solution -> y (want_y)                  osc.h:534-535
+  * wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240, commented out upstream):
+    a model whose YAML switches them on takes the per-env wheel directions (wheel_dir)
   * absl::Status error convention -> OSCError with the osc_status code.
 
 Inputs are torch float64 CUDA tensors already resident in HBM (numpy arrays are copied to the
@@ -31,6 +34,7 @@ class SolveResult:
     status: torch.Tensor       # (nenv,) int32, 0 = converged
     iters: torch.Tensor        # (nenv,) int32, interior-point iterations
     workspace: torch.Tensor | None = None   # device scratch (reduced QP per env)
+    y: torch.Tensor | None = None           # (nenv, dual_rows) dual solution (OSQP convention)
 
 
 class OSCBatchSolver:
@@ -48,12 +52,16 @@ class OSCBatchSolver:
         if max_iter is not None:
             desc.max_iter = int(max_iter)
         self.desc = desc
+        self.wheels = desc.wheel_rows != 0
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             rc = _lib.lib().osc_model_create(ctypes.byref(desc), ctypes.byref(h))
         if rc != 0:
             raise _lib.OSCError("osc_model_create", rc)
         self._h = h
+        rows = ctypes.c_int32()
+        _lib.lib().osc_dual_rows(self._h, ctypes.byref(rows))
+        self.dual_rows = rows.value
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -76,11 +84,12 @@ class OSCBatchSolver:
             raise ValueError(f"{name}: expected shape {shape}, got {tuple(a.shape)}")
         return a
 
-    def alloc_outputs(self, nenv: int, want_x: bool = False):
+    def alloc_outputs(self, nenv: int, want_x: bool = False, want_y: bool = False):
         d = self.dims
         opts = dict(device=self.device)
         tau = torch.empty((nenv, d["nu"]), dtype=torch.float64, **opts)
-        x = torch.empty((nenv, d["n"]), dtype=torch.float64, **opts) if want_x else None
+        x = torch.empty((nenv, d["n"]), dtype=torch.float64, **opts) if (want_x or want_y) else None
+        y = torch.empty((nenv, self.dual_rows), dtype=torch.float64, **opts) if want_y else None
         status = torch.empty((nenv,), dtype=torch.int32, **opts)
         iters = torch.empty((nenv,), dtype=torch.int32, **opts)
         nb = ctypes.c_size_t()
@@ -88,32 +97,49 @@ class OSCBatchSolver:
         if rc != 0:
             raise _lib.OSCError("osc_workspace_bytes", rc)
         ws = torch.empty((max(nb.value // 8, 2),), dtype=torch.float64, **opts)
-        return SolveResult(tau, x, status, iters, ws)
+        return SolveResult(tau, x, status, iters, ws, y)
 
-    def solve_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None) -> SolveResult:
-        """Launch only (no allocation, no host sync): the benchmarked call."""
+    def solve_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None,
+                   wheel_dir=None) -> SolveResult:
+        """Launch only (no allocation, no host sync): the benchmarked call.  osc_batch_solve, or
+        osc_batch_solve_ex when the model has wheel rows or duals are wanted (out.y)."""
         nenv = out.tau.shape[0]
         s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        rc = _lib.lib().osc_batch_solve(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
-                                        ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
-                                        ptr(out.iters), ptr(out.workspace),
-                                        ctypes.c_size_t(0 if out.workspace is None else
-                                                        out.workspace.numel() * 8),
-                                        ctypes.c_void_p(s))
+        wsb = ctypes.c_size_t(0 if out.workspace is None else out.workspace.numel() * 8)
+        if wheel_dir is None and out.y is None:
+            rc = _lib.lib().osc_batch_solve(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
+                                            ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
+                                            ptr(out.iters), ptr(out.workspace), wsb,
+                                            ctypes.c_void_p(s))
+            if rc != 0:
+                raise _lib.OSCError("osc_batch_solve", rc)
+            return out
+        ex = _lib.OscSolveExtras(wheel_dir.data_ptr() if wheel_dir is not None else None,
+                                 out.y.data_ptr() if out.y is not None else None)
+        rc = _lib.lib().osc_batch_solve_ex(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
+                                           ptr(mask), ctypes.byref(ex), ptr(out.tau), ptr(out.x),
+                                           ptr(out.status), ptr(out.iters), ptr(out.workspace), wsb,
+                                           ctypes.c_void_p(s))
         if rc != 0:
-            raise _lib.OSCError("osc_batch_solve", rc)
+            raise _lib.OSCError("osc_batch_solve_ex", rc)
         return out
 
-    def assemble_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None) -> SolveResult:
+    def assemble_into(self, out: SolveResult, M, C, J, b, T, mask, stream=None,
+                      wheel_dir=None) -> SolveResult:
         """First half of solve_into: every env's reduced QP into out.workspace."""
         nenv = out.tau.shape[0]
         s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
-        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
-        rc = _lib.lib().osc_batch_assemble(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
-                                           ptr(mask), ptr(out.workspace),
-                                           ctypes.c_size_t(out.workspace.numel() * 8),
-                                           ctypes.c_void_p(s))
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        wsb = ctypes.c_size_t(out.workspace.numel() * 8)
+        if wheel_dir is None:
+            rc = _lib.lib().osc_batch_assemble(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b),
+                                               ptr(T), ptr(mask), ptr(out.workspace), wsb,
+                                               ctypes.c_void_p(s))
+        else:
+            rc = _lib.lib().osc_batch_assemble_ex(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b),
+                                                  ptr(T), ptr(mask), ptr(wheel_dir),
+                                                  ptr(out.workspace), wsb, ctypes.c_void_p(s))
         if rc != 0:
             raise _lib.OSCError("osc_batch_assemble", rc)
         return out
@@ -183,11 +209,15 @@ class OSCBatchSolver:
                 self._as_dev(T, (nenv, d["ns"], 6), "T"),
                 self._as_dev(mask, (nenv, d["nc"]), "mask"))
 
-    def solve(self, M, C, J, b, T, mask, want_x: bool = False) -> SolveResult:
+    def solve(self, M, C, J, b, T, mask, want_x: bool = False, want_y: bool = False,
+              wheel_dir=None) -> SolveResult:
         args = self.prepare(M, C, J, b, T, mask)
-        out = self.alloc_outputs(int(args[0].shape[0]), want_x)
+        nenv = int(args[0].shape[0])
+        if wheel_dir is not None:
+            wheel_dir = self._as_dev(wheel_dir, (nenv, self.dims["nc"], 6), "wheel_dir")
+        out = self.alloc_outputs(nenv, want_x, want_y)
         with torch.cuda.device(self.device):
-            return self.solve_into(out, *args)
+            return self.solve_into(out, *args, wheel_dir=wheel_dir)
 
 
 def solve_multi_into(jobs, stream=None) -> None:

@@ -14,6 +14,9 @@ Followed line by line (paths relative to /root/reference/operational-space-contr
   * term '<name>_translational_tracking' = sumsqr(ddx_<name>_p - desired_<name>_p), likewise
     rotational; 'torque' = sumsqr(u); 'regularization' = sumsqr(q) (the whole design vector);
   * objective = sum over terms of term * weights_config[key].
+  walter_sr_wheels/autogen/autogen.py:128-240 (the commented-out no-slip design) for
+  wheel_constraints(), with the wheel joint -> dof lookup of :64-94 passed in as
+  wheel_joint_ids_in_nv.
 """
 from __future__ import annotations
 
@@ -74,3 +77,38 @@ def hessian_gradient_at_zero(fun, n: int):
             H[i, j] = H[j, i] = (fun(E[i] + E[j]) - fi[i] - fi[j] + f0) if i != j else \
                 fi[i] + fm[i] - 2.0 * f0
     return H, (fi - fm) / 2.0
+
+
+def wheel_constraints(q, J_wheel_p, J_dot_wheel_p, joint_velocities_current, wheel_radii,
+                      wheel_directions, wheel_joint_ids_in_nv, nv: int):
+    """The no-slip equality constraints exactly as walter_sr_wheels/autogen/autogen.py:185-240
+    writes them (commented out upstream): per wheel i, contact_lin_accel_i = J_p_i @ dv +
+    J_dot_p_i @ joint_velocities_current (:216); longitudinal_slip = dot(contact_lin_accel_i,
+    d_roll_i) - r_wheel * ddq_k (:226); lateral_slip = dot(contact_lin_accel_i, d_lat_i) (:230);
+    appended in that order (:227, :231).  (A wheel without a joint -- index -1 -- has no ddq_k
+    term: the extension osc_qp.WheelRows allows.)"""
+    q = np.asarray(q, dtype=np.float64)
+    dv = q[:nv]
+    num_wheels = len(wheel_radii)
+    wheel_constraints = []
+    for i in range(num_wheels):
+        J_p_i = np.asarray(J_wheel_p)[3 * i:3 * (i + 1), :]
+        J_dot_p_i = np.asarray(J_dot_wheel_p)[3 * i:3 * (i + 1), :]
+        wheel_jnt_dof_idx = wheel_joint_ids_in_nv[i]
+        ddq_k = dv[wheel_jnt_dof_idx] if wheel_jnt_dof_idx >= 0 else 0.0
+        r_wheel = wheel_radii[i]
+        contact_lin_accel_i = J_p_i @ dv + J_dot_p_i @ np.asarray(joint_velocities_current)
+        d_roll_i = np.asarray(wheel_directions)[i, 0:3]
+        d_lat_i = np.asarray(wheel_directions)[i, 3:6]
+        longitudinal_slip = float(np.dot(contact_lin_accel_i, d_roll_i)) - r_wheel * ddq_k
+        wheel_constraints.append(longitudinal_slip)
+        lateral_slip = float(np.dot(contact_lin_accel_i, d_lat_i))
+        wheel_constraints.append(lateral_slip)
+    return np.array(wheel_constraints)
+
+
+def jacobian_value_at_zero(fun, n: int):
+    """Exact for an affine f: jacobian columns f(e_i) - f(0), value f(0)."""
+    f0 = np.asarray(fun(np.zeros(n)))
+    E = np.eye(n)
+    return np.stack([np.asarray(fun(E[i])) - f0 for i in range(n)], axis=1), f0

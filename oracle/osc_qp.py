@@ -27,6 +27,8 @@ Reference citations (paths relative to /root/reference/operational-space-control
   * bounds (u limits, z limits, big_number) ...... unitree_go2/operational_space_controller.h:276-309,
                                                    walter_sr/operational_space_controller.h:309-353
   * torque = x[nv : nv+nu] ....................... unitree_go2/operational_space_controller.h:573
+  * wheel no-slip equality rows (opt-in) .......... walter_sr_wheels/autogen/autogen.py:128-240
+    (commented out upstream), wheel joint -> dof    walter_sr_wheels/autogen/autogen.py:64-94
 """
 from __future__ import annotations
 
@@ -185,9 +187,56 @@ class QPData:
     A: np.ndarray
     l: np.ndarray
     u: np.ndarray
+    Aw: np.ndarray | None = None    # wheel no-slip rows (2 nc x n), when enabled
+    bw: np.ndarray | None = None
 
 
-def build_qp(model: OSCModel, M, C, J, b, T, mask) -> QPData:
+@dataclasses.dataclass
+class WheelRows:
+    """The wheel no-slip equality rows the walter_sr_wheels autogen designs but leaves commented
+    out (walter_sr_wheels/autogen/autogen.py:128-240).  Per wheel i (= contact site i, whose
+    translational Jacobian rows J_p,i and bias J_dot_p,i qd are the contact rows of J and b):
+
+        longitudinal:  d_roll_i . (J_p,i dv + J_dot_p,i qd) - r_i ddq_{k_i} = 0     (:222-227)
+        lateral:       d_lat_i  . (J_p,i dv + J_dot_p,i qd)               = 0     (:229-231)
+
+    stacked after the dynamics rows (:236-239).  k_i = the dof of wheel i's joint
+    (jnt_dofadr of the joint named in wheel_joints_list, :64-94), -1 when the model has no wheel
+    joint (no rolling term).  The directions d_roll, d_lat are per-env inputs (the design's
+    `wheel_directions`, :535-537); r_i is per wheel (`wheel_radii`, :530).  Extension of the
+    design: each wheel's two rows are multiplied by its contact mask, as the reference masks the
+    contact-force bounds (operational_space_controller.h:492-495): a wheel off the ground
+    contributes the trivial rows 0 = 0."""
+    dof: np.ndarray      # (nc,) int
+    radius: np.ndarray   # (nc,)
+
+
+def wheel_rows(model: OSCModel, J, b, mask, wheel: WheelRows, wheel_dir):
+    """(Aw, bw): the 2 nc no-slip rows over x = (dv, u, z) and their right-hand side, in the
+    CasADi convention of the dynamics rows (jacobian at x = 0; beq = -value at x = 0)."""
+    nv, n, nc = model.nv, model.n, model.nc
+    J = np.asarray(J, float).reshape(model.s, nv)
+    b = np.asarray(b, float).reshape(model.s)
+    wd = np.asarray(wheel_dir, float).reshape(nc, 6)
+    mask = np.asarray(mask, float).reshape(nc)
+    r0 = 3 * model.ns - model.nz                     # first contact translational row (osc.h:439)
+    Aw = np.zeros((2 * nc, n))
+    bw = np.zeros(2 * nc)
+    for i in range(nc):
+        Jp, bi = J[r0 + 3 * i:r0 + 3 * i + 3], b[r0 + 3 * i:r0 + 3 * i + 3]
+        d_roll, d_lat = wd[i, :3], wd[i, 3:]
+        Aw[2 * i, :nv] = d_roll @ Jp
+        if wheel.dof[i] >= 0:
+            Aw[2 * i, wheel.dof[i]] -= wheel.radius[i]
+        Aw[2 * i + 1, :nv] = d_lat @ Jp
+        bw[2 * i], bw[2 * i + 1] = -(d_roll @ bi), -(d_lat @ bi)
+        Aw[2 * i:2 * i + 2] *= mask[i]
+        bw[2 * i:2 * i + 2] *= mask[i]
+    return Aw, bw
+
+
+def build_qp(model: OSCModel, M, C, J, b, T, mask, wheel: WheelRows | None = None,
+             wheel_dir=None) -> QPData:
     """Closed-form restatement of the six CasADi functions + OSQP stacking for ONE env.
 
     H = hessian(objective) = blockdiag(2 J^T W J + 2 w_reg I, 2 (w_tau + w_reg) I, 2 w_reg I)
@@ -225,14 +274,19 @@ def build_qp(model: OSCModel, M, C, J, b, T, mask) -> QPData:
             Aineq[4 * k + r, c0 + 2] = -mu
     bineq = np.zeros(4 * model.nc)
 
-    A = np.vstack([Aeq, Aineq, np.eye(n)])
+    Aw = bw = None
+    if wheel is not None:   # the design's stacking: [dynamics; wheels] (autogen.py:236-239)
+        Aw, bw = wheel_rows(model, J, b, mask, wheel, wheel_dir)
+    Aeq_all = Aeq if Aw is None else np.vstack([Aeq, Aw])
+    beq_all = beq if bw is None else np.concatenate([beq, bw])
+    A = np.vstack([Aeq_all, Aineq, np.eye(n)])
     z_lb = np.tile([-OSQP_INFTY, -OSQP_INFTY, 0.0], model.nc)
     z_ub = np.tile([OSQP_INFTY, OSQP_INFTY, BIG_NUMBER], model.nc)
     mrep = np.repeat(mask, 3)
-    l = np.concatenate([beq, np.full(4 * model.nc, -OSQP_INFTY), np.full(nv, -OSQP_INFTY),
+    l = np.concatenate([beq_all, np.full(4 * model.nc, -OSQP_INFTY), np.full(nv, -OSQP_INFTY),
                         model.u_lb, z_lb * mrep])
-    u = np.concatenate([beq, bineq, np.full(nv, OSQP_INFTY), model.u_ub, z_ub * mrep])
-    return QPData(H, f, Aeq, beq, Aineq, bineq, A, l, u)
+    u = np.concatenate([beq_all, bineq, np.full(nv, OSQP_INFTY), model.u_ub, z_ub * mrep])
+    return QPData(H, f, Aeq, beq, Aineq, bineq, A, l, u, Aw, bw)
 
 
 def torque(model: OSCModel, x: np.ndarray) -> np.ndarray:

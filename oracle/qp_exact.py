@@ -46,6 +46,10 @@ def _constraints(qp: QPData):
     for i in range(m):
         lo, hi = qp.l[i], qp.u[i]
         if lo == hi:
+            if i < m - n and not qp.A[i].any():
+                # a trivial row 0 = 0 (the no-slip rows of a wheel off the ground): implied
+                assert lo == 0.0, "inconsistent zero row"
+                continue
             eq.append(i)
             continue
         support = np.nonzero(qp.A[i])[0]
@@ -64,7 +68,7 @@ def _constraints(qp: QPData):
 def _feasible_start(model: OSCModel, qp: QPData, M, C, J):
     """Strictly interior point for every one-sided row (u mid-box, z = (0, 0, fz0))."""
     nv, nu, nz = model.nv, model.nu, model.nz
-    off_u = nv + 4 * model.nc + nv
+    off_u = qp.A.shape[0] - model.n + nv
     off_z = off_u + nu
     lu, uu = qp.l[off_u:off_u + nu], qp.u[off_u:off_u + nu]
     u0 = np.where((lu < 0) & (uu > 0), 0.0, 0.5 * (lu + uu))
@@ -76,6 +80,25 @@ def _feasible_start(model: OSCModel, qp: QPData, M, C, J):
     rhs = b_matrix(model) @ u0 + contact_jacobian(model, J) @ z0 - np.asarray(C).reshape(-1)
     dv0 = np.linalg.solve(np.asarray(M).reshape(nv, nv), rhs)
     return np.concatenate([dv0, u0, z0])
+
+
+def _phase1_start(qp: QPData, eq, ineq):
+    """A point that satisfies every equality row and is as deep inside the one-sided rows as the
+    LP  max t  s.t.  A_eq x = b_eq,  s_i a_i x + t <= bound_i,  t <= 1  can make it (HiGHS).  Used
+    when equality rows beyond the dynamics (wheel no-slip rows) constrain dv, so the dynamics-only
+    start of _feasible_start no longer applies."""
+    from scipy.optimize import linprog
+    n = qp.A.shape[1]
+    c = np.zeros(n + 1)
+    c[-1] = -1.0
+    A_ub = np.array([np.append(sg * qp.A[i], 1.0) for (i, sg, _) in ineq])
+    b_ub = np.array([bd for (_, _, bd) in ineq])
+    A_eq = np.hstack([qp.A[eq], np.zeros((len(eq), 1))])
+    res = linprog(c, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=qp.u[eq],
+                  bounds=[(None, None)] * n + [(None, 1.0)], method="highs")
+    if res.status != 0 or res.x[-1] <= 0.0:
+        raise RuntimeError(f"QP has no strictly feasible point (phase-1 status {res.status})")
+    return res.x[:n]
 
 
 def kkt_certificate(qp: QPData, x: np.ndarray, y: np.ndarray) -> dict:
@@ -122,7 +145,7 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
     n = model.n
     eq, ineq = _constraints(qp)
     A = qp.A
-    x = _feasible_start(model, qp, M, C, J)
+    x = (_feasible_start(model, qp, M, C, J) if qp.Aw is None else _phase1_start(qp, eq, ineq))
     # sanity: strictly feasible for all one-sided rows
     for (i, sg, bd) in ineq:
         assert sg * (A[i] @ x) < bd, "start point not strictly feasible"

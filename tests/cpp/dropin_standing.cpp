@@ -87,14 +87,14 @@ int lifecycle(const char* xml) {
 }
 
 int run(const char* xml, const char* qpos_path, const char* qvel_path) {
-  const std::vector<double> qpos_file = read_doubles(qpos_path);
-  const std::vector<double> qvel_file = read_doubles(qvel_path);
+  std::vector<double> qpos_file = read_doubles(qpos_path);   // mutable, as mj_data->qpos
+  std::vector<double> qvel_file = read_doubles(qvel_path);
   if (static_cast<int>(qpos_file.size()) != model::nq_size ||
       static_cast<int>(qvel_file.size()) != model::nv_size) {
     std::fprintf(stderr, "state files: %zu / %zu values\n", qpos_file.size(), qvel_file.size());
     return 2;
   }
-  const std::vector<double> qfrc(model::nv_size, 0.0);
+  std::vector<double> qfrc(model::nv_size, 0.0);
   std::filesystem::path osc_model_path = xml;
 
   // ---- examples/standing.cc:86-117 ----

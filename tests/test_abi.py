@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.osc_abi_version() == 1
+    assert L.osc_abi_version() == 2
     assert L.osc_status_string(2) == b"OSC_ERR_UNSUPPORTED_DIMS"
 
 
@@ -73,6 +73,42 @@ def test_reads_reference_yaml_files(robot, rel):
         _lib.lib().osc_model_destroy(h)
 
 
+def test_wheel_no_slip_yaml_keys(tmp_path):
+    """The opt-in wheel rows (walter_sr_wheels/autogen/autogen.py:64-94, 128-240) come from three
+    optional YAML keys; the reference's own configs (no such keys) leave them off."""
+    from osc_amd.robots import config_path
+    from osc_amd.synth import WALTER_WHEEL_DOFS, WHEEL_RADIUS
+    assert _lib.desc_from_yaml("walter_sr_wheels").wheel_rows == 0
+    d = _lib.desc_from_yaml("walter_sr_wheels", os.path.join(
+        os.path.dirname(config_path("walter_sr_wheels")), "walter_sr_wheels_noslip_config.yaml"))
+    assert d.wheel_rows == 1
+    assert list(d.wheel_dof[:8]) == WALTER_WHEEL_DOFS and list(d.wheel_radius[:8]) == [WHEEL_RADIUS] * 8
+    base = open(config_path("walter_sr_wheels")).read()
+    for extra, ok in [("wheel_no_slip: true\nwheel_radius: [1, 2, 3, 4, 5, 6, 7, 8]\n"
+                       "wheel_dofs: [-1, -1, 6, 7, 8, 9, 10, 11]\n", True),
+                      ("wheel_no_slip: true\nwheel_radius: 0.1\nwheel_dofs: [1, 2]\n", False),
+                      ("wheel_no_slip: true\nwheel_radius: 0.1\n"
+                       "wheel_dofs: [0, 0, 0, 0, 0, 0, 0, 14]\n", False),
+                      ("wheel_no_slip: maybe\n", False),
+                      ("wheel_no_slip: false\n", True)]:
+        f = tmp_path / "w.yaml"
+        f.write_text(base + extra)
+        if ok:
+            _lib.desc_from_yaml("walter_sr_wheels", str(f))
+        else:
+            with pytest.raises(_lib.OSCError):
+                _lib.desc_from_yaml("walter_sr_wheels", str(f))
+    d = _lib.desc_from_yaml("walter_sr_wheels", str(tmp_path / "w.yaml"))
+    assert d.wheel_rows == 0
+    # models with wheel rows: only the WaLTER dimensions have a kernel; bad dof indices refused
+    h = ctypes.c_void_p()
+    g = _lib.desc_from_yaml("unitree_go2")
+    g.wheel_rows = 1
+    assert _lib.lib().osc_model_create(ctypes.byref(g), ctypes.byref(h)) == 2
+    d.wheel_rows, d.wheel_dof[0] = 1, 14
+    assert _lib.lib().osc_model_create(ctypes.byref(d), ctypes.byref(h)) == 1
+
+
 def test_error_codes():
     L = _lib.lib()
     d = _lib.OscModelDesc()
@@ -88,6 +124,10 @@ def test_error_codes():
     assert L.osc_batch_solve(None, 1, *([None] * 10), None, 0, None) == 1
     assert L.osc_batch_assemble(None, 1, *([None] * 6), None, 0, None) == 1
     assert L.osc_batch_solve_assembled(None, 1, *([None] * 5), None, 0, None) == 1
+    assert L.osc_batch_solve_ex(None, 1, *([None] * 6), None, *([None] * 4), None, 0, None) == 1
+    assert L.osc_batch_assemble_ex(None, 1, *([None] * 7), None, 0, None) == 1
+    rows = ctypes.c_int32()
+    assert L.osc_dual_rows(None, ctypes.byref(rows)) == 1
     assert L.osc_pd_base_targets(1, 5, *([None] * 5), 0, None, 0, None, None, None) == 1
     assert L.osc_contact_mask_from_contacts(1, 4, 2, None, None, 0, None, None, None) == 1
     assert L.osc_model_destroy(None) == 1

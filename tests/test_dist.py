@@ -71,7 +71,7 @@ class _StubSolver:
                                      status=torch.zeros(nenv, dtype=torch.int32),
                                      iters=torch.full((nenv,), 10, dtype=torch.int32))
 
-    def solve_into(self, out, *inputs):
+    def solve_into(self, out, *inputs, stream=None):
         out.tau.zero_()
 
     def assemble_into(self, out, M, C, J, b, T, mask):
@@ -81,6 +81,11 @@ class _StubSolver:
         out.status.zero_()
 
 
+def _stub_multi(jobs, stream=None):
+    for solver, out, inputs in jobs:
+        solver.solve_into(out, *inputs)
+
+
 def _bench_worker(rank, world, port, out_dir):
     import json
     import bench
@@ -88,10 +93,14 @@ def _bench_worker(rank, world, port, out_dir):
                             world_size=world)
     try:
         args = bench.parse_args(["--gpus", str(world), "--steps", "3", "--warmup", "1",
-                                 "--nenv-per-gpu", "24", "--traffic-json", "/nonexistent"])
+                                 "--nenv-per-gpu", "24", "--traffic-json", "/nonexistent",
+                                 "--north-star-envs", "50", "--mixed-envs", "8"])
         dev = torch.device("cpu")
+        clock = bench.DeviceClock(dev)
         line, _, inputs = bench.run_headline(args, world, rank, dev, lambda: barrier(world),
-                                             _StubSolver, bench.DeviceClock(dev))
+                                             _StubSolver, clock)
+        bench.attach_multi_gpu_objects(args, world, rank, dev, lambda: barrier(world), _StubSolver,
+                                       clock, line, multi_fn=_stub_multi)
         np.save(os.path.join(out_dir, f"M{rank}.npy"), inputs[0].numpy())
         if rank == 0:
             with open(os.path.join(out_dir, "line.json"), "w") as fh:
@@ -115,6 +124,15 @@ def test_bench_rank_path_two_gloo_ranks(tmp_path):
     assert line["converged_frac"] == 1.0
     # independent shards: each rank drew its own environments
     assert not np.array_equal(np.load(tmp_path / "M0.npy"), np.load(tmp_path / "M1.npy"))
+    # BASELINE north_star: Go2 at a fixed GLOBAL batch split over the ranks (50 = 25 + 25)
+    ns = line["north_star"]
+    assert ns["global_envs"] == 50 and ns["envs_per_gpu"] == 25 and ns["n_gpus"] == 2
+    assert ns["converged_frac"] == 1.0 and ns["target"] == 1e6
+    assert abs(ns["value"] - 50 * 3 / (ns["ms_per_step"] * 3 / 1e3)) <= 1e-6 * ns["value"]
+    # configs[4]: 8 Go2 + 8 WaLTER per rank through the multi-model call
+    mx = line["mixed"]
+    assert mx["config"]["global_envs"] == 2 * 2 * 8 and mx["config"]["envs_per_gpu"] == 16
+    assert mx["converged_frac"] == 1.0
 
 
 def test_bench_launcher(monkeypatch):

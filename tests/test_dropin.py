@@ -101,3 +101,22 @@ def test_standing_loop_matches_oracle(gpu, robot, tmp_path):
     assert np.array_equal(np.asarray(out["solution"])[model.nv:model.nv + model.nu], tau)
     if robot == "unitree_go2":
         assert np.abs(T[0]).max() > 0 and np.all(T[1:] == 0)   # the base PD row only
+
+
+def test_eigen_stub_is_as_strict_as_eigen(tmp_path):
+    """The stub rejects what real Eigen rejects for the calls the harness makes: Map<M> needs
+    mutable storage (examples/standing.cc:90-92 maps mj_data->qpos, a double*); read-only storage
+    needs Map<const M>."""
+    stub = os.path.join(REPO, "tests", "cpp", "stubs")
+    cases = {"mutable": ("double a[3] = {1, 2, 3};\n"
+                         "Eigen::Matrix<double, 3, 1> v = Eigen::Map<Eigen::Matrix<double, 3, 1>>(a);", 0),
+             "const_view": ("const double a[3] = {1, 2, 3};\n"
+                            "Eigen::Matrix<double, 3, 1> v = Eigen::Map<const Eigen::Matrix<double, 3, 1>>(a);", 0),
+             "const_into_mutable": ("const double a[3] = {1, 2, 3};\n"
+                                    "Eigen::Matrix<double, 3, 1> v = Eigen::Map<Eigen::Matrix<double, 3, 1>>(a);", 1)}
+    for name, (body, fails) in cases.items():
+        src = tmp_path / f"{name}.cpp"
+        src.write_text("#include <Eigen/Dense>\nint main() {\n" + body + "\nreturn v(0) > 0 ? 0 : 1;\n}\n")
+        r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", stub, str(src)],
+                           capture_output=True, text=True)
+        assert (r.returncode != 0) == bool(fails), (name, r.stderr[-500:])

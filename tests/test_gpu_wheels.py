@@ -1,0 +1,282 @@
+"""GPU tests of the opt-in wheel no-slip rows, the dual solution export, the
+UNREFINED status, and the bitwise-unchanged feature-off path.
+
+Wheel rows: walter_sr_wheels/autogen/autogen.py:128-240 (commented out in the reference), joint
+lookup :64-94; oracle: oracle/osc_qp.py wheel_rows + oracle/qp_exact.py (phase-1 start, active
+set, KKT certificate), pinned to the literal design by tests/test_oracle.py.  Tolerances as
+tests/test_gpu_parity.py: normwise <= 1e-9, elementwise (above 1 % of the norm) <= 1e-7 against
+the certified exact optimum; the rows themselves hold to 1e-9 at the returned x.
+
+Duals (the reference's OsqpSolver::dual_solution, operational_space_controller.h:534-535):
+checked by the OSQP-form KKT certificate of (x, y) on EVERY env of the BASELINE-size batches,
+batched in torch on the GPU (stated tolerances below).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from osc_amd.robots import config_path, dims
+from osc_amd.synth import SEED_BASE, WALTER_WHEEL_DOFS, WHEEL_RADIUS, generate, wheel_directions
+from osc_qp import BIG_NUMBER, WheelRows, build_qp, load_model, torque
+from qp_exact import solve_exact
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NOSLIP_YAML = os.path.join(os.path.dirname(config_path("walter_sr_wheels")),
+                           "walter_sr_wheels_noslip_config.yaml")
+NORM_ACH, ELEM_ACH = 1e-9, 1e-7
+# KKT certificate of the GPU's (x, y), each residual scaled as oracle/qp_exact.kkt_certificate
+KKT_STAT, KKT_PRIMAL, KKT_DUAL, KKT_COMP = 1e-8, 1e-9, 1e-9, 1e-9
+
+_solvers = {}
+
+
+def solver(key):
+    from osc_amd.solver import OSCBatchSolver
+    if key not in _solvers:
+        _solvers[key] = (OSCBatchSolver("walter_sr_wheels", NOSLIP_YAML) if key == "noslip"
+                         else OSCBatchSolver(key))
+    return _solvers[key]
+
+
+def _rel_errors(tau, ref):
+    tau, ref = np.asarray(tau), np.asarray(ref)
+    nrm = np.maximum(np.abs(ref).max(axis=-1, keepdims=True), 1.0)
+    normwise = (np.abs(tau - ref) / nrm).max(axis=-1)
+    big = np.abs(ref) >= 1e-2 * np.abs(ref).max(axis=-1, keepdims=True)
+    elem = np.where(big, np.abs(tau - ref) / np.maximum(np.abs(ref), 1e-300), 0.0).max(axis=-1)
+    return normwise, elem
+
+
+def _wheel():
+    return WheelRows(dof=np.array(WALTER_WHEEL_DOFS), radius=np.full(8, WHEEL_RADIUS))
+
+
+def test_feature_off_bitwise_unchanged(gpu):
+    """Models without wheel rows -- the feature-off path -- give bitwise the results of the
+    round-2 build (tests/golden/feature_off_hashes.json, made by
+    tests/golden/make_feature_off_hashes.py with that library)."""
+    from golden.make_feature_off_hashes import fingerprint
+    ref = json.load(open(os.path.join(HERE, "golden", "feature_off_hashes.json")))
+    for c in ref["cases"]:
+        d = generate(c["robot"], c["nenv"], c["seed"], c["scenario"], c["mask"])
+        assert fingerprint(solver(c["robot"]), d) == c["sha256"], c
+
+
+@pytest.mark.parametrize("scenario,mask_mode,seed", [("standing", "ones", 81),
+                                                      ("tumbling", "bernoulli", 82)])
+def test_wheel_rows_vs_oracle(gpu, scenario, mask_mode, seed):
+    """64 fresh envs with the no-slip rows on: torques against the exact oracle optimum, the
+    rows hold at the returned design vector, every env converged and refined."""
+    nenv = 64
+    model = load_model("walter_sr_wheels")
+    wheel = _wheel()
+    d = generate("walter_sr_wheels", nenv, SEED_BASE + seed, scenario, mask_mode)
+    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + seed + 1)
+    res = solver("noslip").solve(**d, want_x=True, wheel_dir=wd)
+    torch.cuda.synchronize()
+    assert (res.status.cpu().numpy() == 0).all(), res.status
+    x = res.x.cpu().numpy()
+    ref, viol = [], []
+    for e in range(nenv):
+        args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        qp = build_qp(model, *args, wheel, wd[e])
+        ref.append(torque(model, solve_exact(model, qp, *args[:3]).x))
+        viol.append(np.abs(qp.Aw @ x[e] - qp.bw).max() / (1.0 + np.abs(qp.bw).max()))
+    nw, el = _rel_errors(res.tau.cpu().numpy(), np.array(ref))
+    assert nw.max() <= NORM_ACH and el.max() <= ELEM_ACH, (nw.max(), el.max(), int(np.argmax(nw)))
+    assert max(viol) <= 1e-9, max(viol)
+
+
+def test_wheel_rows_that_vanish_change_nothing(gpu, tmp_path):
+    """Rows that vanish (zero directions, no wheel joints) leave the reference's QP: the
+    wheel-row kernel then agrees with the feature-off kernel to rounding."""
+    from osc_amd.solver import OSCBatchSolver
+    text = open(NOSLIP_YAML).read().replace("wheel_dofs: [7, 7, 9, 9, 11, 11, 13, 13]",
+                                            "wheel_dofs: [-1, -1, -1, -1, -1, -1, -1, -1]")
+    (tmp_path / "nodof.yaml").write_text(text)
+    d = generate("walter_sr_wheels", 128, SEED_BASE + 83, "tumbling", "bernoulli")
+    off = solver("walter_sr_wheels").solve(**d)
+    on = OSCBatchSolver("walter_sr_wheels", str(tmp_path / "nodof.yaml")).solve(
+        **d, wheel_dir=np.zeros((128, 8, 6)))
+    torch.cuda.synchronize()
+    assert (on.status.cpu().numpy() == 0).all()
+    nw, _ = _rel_errors(on.tau.cpu().numpy(), off.tau.cpu().numpy())
+    assert nw.max() <= 1e-10, nw.max()
+
+
+def test_wheel_model_entry_points(gpu):
+    """A wheel model needs its directions: the plain entries refuse it, warm start and the
+    multi-model call are not compiled for it, split assemble + solve equals the fused call."""
+    from osc_amd import _lib
+    s = solver("noslip")
+    d = generate("walter_sr_wheels", 8, SEED_BASE + 84, "tumbling", "bernoulli")
+    wd = torch.from_numpy(wheel_directions("walter_sr_wheels", d, _wheel().dof, _wheel().radius,
+                                           SEED_BASE + 85)).cuda()
+    args = s.prepare(**d)
+    out = s.alloc_outputs(8, want_x=True)
+    with pytest.raises(_lib.OSCError) as e:
+        s.solve_into(out, *args)
+    assert e.value.code == 1
+    warm = s.alloc_warm_state(8)
+    with pytest.raises(_lib.OSCError) as e:
+        s.solve_warm_into(out, warm, *args)
+    assert e.value.code == 2
+    s.solve_into(out, *args, wheel_dir=wd)
+    split = s.alloc_outputs(8, want_x=True)
+    s.assemble_into(split, *args[:5], args[5], wheel_dir=wd)
+    s.solve_assembled_into(split, args[5])
+    torch.cuda.synchronize()
+    assert torch.equal(out.tau, split.tau) and torch.equal(out.x, split.x)
+
+
+# ---------------------------------------------------------------------------- duals / KKT
+def _batched_qp(robot, M, C, J, b, T, mask, wheel=None, wd=None):
+    """The reference QP of oracle/osc_qp.build_qp for a whole batch, on the GPU (torch fp64):
+    H, f, A = [Aeq (; Aw); Aineq; I], l, u."""
+    m = load_model(robot)
+    nv, nu, nz, n, nc, ns = m.nv, m.nu, m.nz, m.n, m.nc, m.ns
+    dev, E = M.device, M.shape[0]
+    W = torch.as_tensor(np.concatenate([np.repeat(m.w_pos, 3), np.repeat(m.w_rot, 3)]), device=dev)
+    t = torch.cat([T[:, :, 0:3].reshape(E, -1), T[:, :, 3:6].reshape(E, -1)], dim=1)
+    H = torch.zeros(E, n, n, dtype=torch.float64, device=dev)
+    JW = J.transpose(1, 2) * W
+    H[:, :nv, :nv] = 2.0 * JW @ J + 2.0 * m.w_reg * torch.eye(nv, device=dev, dtype=torch.float64)
+    idx = torch.arange(nv, n, device=dev)
+    H[:, idx, idx] = torch.where(idx < nv + nu, 2.0 * (m.w_torque + m.w_reg), 2.0 * m.w_reg).double()
+    f = torch.zeros(E, n, dtype=torch.float64, device=dev)
+    f[:, :nv] = 2.0 * torch.einsum("eij,ej->ei", JW, b - t)
+    r0 = 3 * ns - nz
+    Jc = J[:, r0:3 * ns, :].transpose(1, 2)
+    Aeq = torch.zeros(E, nv, n, dtype=torch.float64, device=dev)
+    Aeq[:, :, :nv] = M
+    Aeq[:, nv - nu:, nv:nv + nu] = -torch.eye(nu, device=dev, dtype=torch.float64)
+    Aeq[:, :, nv + nu:] = -Jc
+    rows, lo, hi = [Aeq], [-C], [-C]
+    if wheel is not None:
+        Aw = torch.zeros(E, 2 * nc, n, dtype=torch.float64, device=dev)
+        bw = torch.zeros(E, 2 * nc, dtype=torch.float64, device=dev)
+        for i in range(nc):
+            Jp, bi = J[:, r0 + 3 * i:r0 + 3 * i + 3, :], b[:, r0 + 3 * i:r0 + 3 * i + 3]
+            for side in range(2):
+                dvec = wd[:, i, 3 * side:3 * side + 3]
+                Aw[:, 2 * i + side, :nv] = torch.einsum("ec,ecj->ej", dvec, Jp)
+                if side == 0 and wheel.dof[i] >= 0:
+                    Aw[:, 2 * i, wheel.dof[i]] -= wheel.radius[i]
+                bw[:, 2 * i + side] = -(dvec * bi).sum(dim=1)
+            Aw[:, 2 * i:2 * i + 2] *= mask[:, i, None, None]
+            bw[:, 2 * i:2 * i + 2] *= mask[:, i, None]
+        rows.append(Aw)
+        lo.append(bw)
+        hi.append(bw)
+    Ain = torch.zeros(E, 4 * nc, n, dtype=torch.float64, device=dev)
+    for k in range(nc):
+        for r, (sx, sy) in enumerate(((1, 1), (-1, 1), (1, -1), (-1, -1))):
+            Ain[:, 4 * k + r, nv + nu + 3 * k:nv + nu + 3 * k + 3] = torch.tensor(
+                [sx, sy, -m.mu], dtype=torch.float64, device=dev)
+    rows += [Ain, torch.eye(n, dtype=torch.float64, device=dev).expand(E, n, n)]
+    inf = 1e30
+    mrep = mask.repeat_interleave(3, dim=1)
+    zlb = torch.tensor([-inf, -inf, 0.0] * nc, dtype=torch.float64, device=dev)
+    zub = torch.tensor([inf, inf, BIG_NUMBER] * nc, dtype=torch.float64, device=dev)
+    full = lambda v: torch.full((E, v[0]), v[1], dtype=torch.float64, device=dev)
+    lo += [full((4 * nc, -inf)), full((nv, -inf)),
+           torch.as_tensor(m.u_lb, device=dev).expand(E, nu), zlb * mrep]
+    hi += [full((4 * nc, 0.0)), full((nv, inf)),
+           torch.as_tensor(m.u_ub, device=dev).expand(E, nu), zub * mrep]
+    return H, f, torch.cat(rows, dim=1), torch.cat(lo, dim=1), torch.cat(hi, dim=1)
+
+
+def _kkt(H, f, A, l, u, x, y):
+    """Per-env residuals as oracle/qp_exact.kkt_certificate, batched."""
+    Ax = torch.einsum("emn,en->em", A, x)
+    grad = torch.einsum("eij,ej->ei", H, x) + f
+    Aty = torch.einsum("emn,em->en", A, y)
+    stat = (grad + Aty).abs().amax(dim=1)
+    scale_d = 1.0 + torch.maximum(grad.abs().amax(dim=1), Aty.abs().amax(dim=1))
+    lo_fin, hi_fin = l > -1e20, u < 1e20
+    viol = torch.maximum(torch.where(hi_fin, Ax - u, -1e300), torch.where(lo_fin, l - Ax, -1e300))
+    viol = viol.clamp_min(0.0).amax(dim=1)
+    bnd = (torch.where(hi_fin, u.abs(), 0.0) + torch.where(lo_fin, l.abs(), 0.0)).amax(dim=1)
+    scale_p = 1.0 + torch.maximum(Ax.abs().amax(dim=1), bnd)
+    yp, ym = y.clamp_min(0.0), (-y).clamp_min(0.0)
+    dual = torch.maximum(torch.where(hi_fin, 0.0, yp).amax(dim=1),
+                         torch.where(lo_fin, 0.0, ym).amax(dim=1))
+    comp = torch.maximum((yp * torch.where(hi_fin, u - Ax, 0.0)).abs(),
+                         (ym * torch.where(lo_fin, Ax - l, 0.0)).abs()).amax(dim=1)
+    return dict(stationarity=stat / scale_d, primal=viol / scale_p, dual=dual / scale_d,
+                complementarity=comp / (scale_d * scale_p))
+
+
+def _certify(cert, where):
+    for k, tol in (("stationarity", KKT_STAT), ("primal", KKT_PRIMAL), ("dual", KKT_DUAL),
+                   ("complementarity", KKT_COMP)):
+        v = cert[k]
+        assert v.max().item() <= tol, (where, k, v.max().item(), int(v.argmax().item()))
+
+
+@pytest.mark.parametrize("robot,nenv,scenario,mask_mode", [
+    ("unitree_go2", 65536, "tumbling", "bernoulli"),     # BASELINE north-star batch
+    ("walter_sr", 8192, "tumbling", "bernoulli"),        # BASELINE configs[3]
+    ("unitree_go2", 4096, "standing", "ones"),           # BASELINE configs[1]
+])
+def test_full_size_kkt_certificate(gpu, robot, nenv, scenario, mask_mode):
+    """Optimality of EVERY env of a BASELINE-size batch, not only feasibility: the exported
+    duals y with the primal x satisfy the OSQP-form KKT conditions of the reference QP
+    (stationarity H x + f + A'y = 0, primal feasibility, dual sign on one-sided rows,
+    complementarity), each scaled as oracle/qp_exact.kkt_certificate."""
+    s = solver(robot)
+    d = generate(robot, nenv, SEED_BASE + 9, scenario, mask_mode)
+    args = s.prepare(**d)
+    out = s.alloc_outputs(nenv, want_y=True)
+    s.solve_into(out, *args)
+    torch.cuda.synchronize()
+    st = out.status.cpu().numpy()
+    assert (st == 0).all(), np.bincount(st)
+    _certify(_kkt(*_batched_qp(robot, *args), out.x, out.y), robot)
+    # the duals leave the torques and the design vector bitwise as the plain solve returns them
+    ref = s.alloc_outputs(nenv, want_x=True)
+    s.solve_into(ref, *args)
+    torch.cuda.synchronize()
+    assert torch.equal(ref.tau, out.tau) and torch.equal(ref.x, out.x)
+
+
+def test_wheel_rows_kkt_certificate(gpu):
+    """The same certificate with the wheel rows in A (their multipliers exported too)."""
+    wheel = _wheel()
+    s = solver("noslip")
+    nenv = 2048
+    d = generate("walter_sr_wheels", nenv, SEED_BASE + 86, "tumbling", "bernoulli")
+    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + 87)
+    args = s.prepare(**d)
+    wdt = torch.from_numpy(wd).cuda()
+    out = s.alloc_outputs(nenv, want_y=True)
+    s.solve_into(out, *args, wheel_dir=wdt)
+    torch.cuda.synchronize()
+    assert (out.status.cpu().numpy() == 0).all()
+    _certify(_kkt(*_batched_qp("walter_sr_wheels", *args, wheel, wdt), out.x, out.y), "wheels")
+
+
+def test_rejected_refinement_is_reported(gpu, monkeypatch):
+    """An env whose full-space refinement is rejected keeps the interior point's iterate and is
+    reported as OSC_SOLVE_UNREFINED (3), not OK; its torques are only as accurate as the
+    interior point's stop (Go2 eps_mu 1e-9: ~1e-5 normwise)."""
+    from osc_amd.solver import OSCBatchSolver
+    monkeypatch.setenv("OSC_REFINE_MAX_MOVE", "0")   # every refinement moves y: all rejected
+    s = OSCBatchSolver("unitree_go2")
+    monkeypatch.delenv("OSC_REFINE_MAX_MOVE")
+    d = generate("unitree_go2", 64, SEED_BASE + 88, "tumbling", "bernoulli")
+    res = s.solve(**d)
+    good = solver("unitree_go2").solve(**d)
+    torch.cuda.synchronize()
+    st = res.status.cpu().numpy()
+    assert (st == 3).all(), np.bincount(st)
+    assert (good.status.cpu().numpy() == 0).all()
+    nw, _ = _rel_errors(res.tau.cpu().numpy(), good.tau.cpu().numpy())
+    assert nw.max() <= 1e-4 and nw.max() > 0.0, nw.max()

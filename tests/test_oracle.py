@@ -173,3 +173,63 @@ def test_closed_form_equals_literal_autogen_objective(robot):
         scale = np.abs(qp.H).max()
         assert np.abs(H - qp.H).max() <= 1e-9 * scale, np.abs(H - qp.H).max() / scale
         assert np.abs(g - qp.f).max() <= 1e-9 * max(np.abs(qp.f).max(), 1.0)
+
+
+def _wheel_setup(robot="walter_sr_wheels"):
+    from osc_qp import WheelRows
+    from osc_amd.synth import WALTER_WHEEL_DOFS, WHEEL_RADIUS
+    model = load_model(robot)
+    wheel = WheelRows(dof=np.array(WALTER_WHEEL_DOFS), radius=np.full(model.nc, WHEEL_RADIUS))
+    return model, wheel
+
+
+def test_wheel_rows_equal_literal_design():
+    """The no-slip rows of osc_qp.wheel_rows against the constraints written exactly as the
+    commented design in walter_sr_wheels/autogen/autogen.py:185-240 writes them (an affine map
+    of the design vector: its jacobian and value at x = 0 give Aeq and -beq, the CasADi
+    convention of the dynamics rows, autogen.py:274-287).  The Jacobian-dot bias the design
+    forms from J_dot_wheel_p @ joint_velocities_current is the contact rows of b."""
+    import autogen_literal as lit
+    from osc_amd.synth import SEED_BASE, generate
+    model, wheel = _wheel_setup()
+    nc, nv, r0 = model.nc, model.nv, 3 * model.ns - model.nz
+    rng = np.random.default_rng(SEED_BASE + 71)
+    d = generate(model.name, 2, SEED_BASE + 71, "tumbling", "ones")
+    for e in range(2):
+        M, C, J, b, T, mask = (d[k][e].copy() for k in ("M", "C", "J", "b", "T", "mask"))
+        Jdot = rng.standard_normal((3 * nc, nv))
+        qd = rng.standard_normal(nv)
+        b[r0:r0 + 3 * nc] = Jdot @ qd
+        wd = rng.standard_normal((nc, 6))
+        qp = build_qp(model, M, C, J, b, T, mask, wheel, wd)
+        Jw, f0 = lit.jacobian_value_at_zero(
+            lambda x: lit.wheel_constraints(x, J[r0:r0 + 3 * nc], Jdot, qd, wheel.radius, wd,
+                                            wheel.dof, nv), model.n)
+        assert np.abs(qp.Aw - Jw).max() <= 1e-12 * np.abs(Jw).max()
+        assert np.abs(qp.bw + f0).max() <= 1e-12 * max(np.abs(f0).max(), 1.0)
+        # stacked after the dynamics rows, as equality rows (autogen.py:236-239)
+        assert np.array_equal(qp.A[nv:nv + 2 * nc], qp.Aw)
+        assert np.array_equal(qp.l[nv:nv + 2 * nc], qp.bw) and np.array_equal(qp.u[nv:nv + 2 * nc], qp.bw)
+    # a wheel off the ground (mask 0) contributes the trivial rows 0 = 0
+    mask = np.ones(nc)
+    mask[[1, 6]] = 0.0
+    qp = build_qp(model, M, C, J, b, T, mask, wheel, wd)
+    assert not qp.Aw[[2, 3, 12, 13]].any() and not qp.bw[[2, 3, 12, 13]].any()
+
+
+def test_wheel_qp_exact_optimum_certified():
+    """With the no-slip rows the oracle's exact solve (phase-1 LP start, active set, KKT
+    refinement) certifies at 1e-9 and the rows hold at the optimum; the optimum moves away from
+    the wheel-free one (the rows bind)."""
+    from osc_amd.synth import SEED_BASE, generate, wheel_directions
+    model, wheel = _wheel_setup()
+    d = generate(model.name, 3, SEED_BASE + 72, "tumbling", "bernoulli")
+    wd = wheel_directions(model.name, d, wheel.dof, wheel.radius, SEED_BASE + 73)
+    for e in range(3):
+        args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        qp = build_qp(model, *args, wheel, wd[e])
+        sol = solve_exact(model, qp, *args[:3])
+        assert certified(sol.cert), sol.cert
+        assert np.abs(qp.Aw @ sol.x - qp.bw).max() <= 1e-9 * (1 + np.abs(qp.bw).max())
+        free = solve_exact(model, build_qp(model, *args), *args[:3])
+        assert np.abs(torque(model, free.x) - torque(model, sol.x)).max() > 1e-3
