@@ -16,14 +16,17 @@
  * MuJoCo 3.2.7 semantics (MODULE.bazel.lock:242-247), restated -- MuJoCo is not linked:
  *   free joint: qpos = (position, unit quaternion w x y z), qvel = (world-frame linear velocity
  *   of the body origin, BODY-frame angular velocity); hinge: rotation about the body-frame axis
- *   through the body-frame anchor; mj_fullM includes dof armature; qfrc_bias = inverse dynamics
+ *   through the body-frame anchor; slide: translation along the body-frame axis; ball: rotation
+ *   about the body-frame anchor, body-frame angular velocity; mj_fullM includes dof armature; qfrc_bias = inverse dynamics
  *   at zero joint acceleration (Coriolis, centrifugal, gravity); mj_jac / mj_jacDot of a point
  *   fixed to a body, world frame, rows in the reference's stacking order.
  *
  * The descriptor mirrors mjModel's fields (body_parentid, body_pos, body_quat, jnt_type,
  * jnt_axis, jnt_pos, dof_armature, body_mass, body_ipos, body_iquat, body_inertia, site_bodyid,
  * site_pos, opt.gravity), restricted to at most one joint per body, so a caller with MuJoCo
- * fills it straight from its mjModel.  Bodies are numbered parents first
+ * fills it straight from its mjModel; a MuJoCo body with several joints is
+ * a chain of bodies here, one joint each, the leading ones massless at zero offset (which is how
+ * mj_kinematics composes a body's joints, in order; osc_kin_desc_from_mjcf does this split).  Bodies are numbered parents first
  * (MuJoCo's order) WITHOUT the world body: parent -1 = world.  Dofs follow body order.
  */
 #ifndef OSC_KINEMATICS_H_
@@ -40,9 +43,15 @@ extern "C" {
 #define OSC_KIN_MAX_DOFS 32
 #define OSC_KIN_MAX_SITES 32
 
-/* Joint types: MuJoCo's mjtJoint values (mjJNT_FREE = 0, mjJNT_HINGE = 3); -1 = welded body. */
+/* Joint types: MuJoCo's mjtJoint values (mjJNT_FREE = 0, mjJNT_BALL = 1, mjJNT_SLIDE = 2,
+ * mjJNT_HINGE = 3); -1 = welded body.
+ *   ball:  qpos = unit quaternion (w x y z) of the body relative to its parent frame, rotating
+ *          about the anchor jnt_pos; qvel = body-frame angular velocity (3 dofs);
+ *   slide: qpos = displacement along the body-frame axis; qvel = its rate (1 dof). */
 #define OSC_KIN_JOINT_NONE (-1)
 #define OSC_KIN_JOINT_FREE 0
+#define OSC_KIN_JOINT_BALL 1
+#define OSC_KIN_JOINT_SLIDE 2
 #define OSC_KIN_JOINT_HINGE 3
 
 typedef struct {
@@ -53,8 +62,8 @@ typedef struct {
   int32_t jnt_type[OSC_KIN_MAX_BODIES];            /* OSC_KIN_JOINT_*                          */
   double pos[OSC_KIN_MAX_BODIES][3];               /* body_pos  (parent frame)                 */
   double quat[OSC_KIN_MAX_BODIES][4];              /* body_quat (w, x, y, z)                   */
-  double axis[OSC_KIN_MAX_BODIES][3];              /* jnt_axis  (body frame; hinge)            */
-  double jnt_pos[OSC_KIN_MAX_BODIES][3];           /* jnt_pos   (body frame; hinge anchor)     */
+  double axis[OSC_KIN_MAX_BODIES][3];              /* jnt_axis  (body frame; hinge, slide)     */
+  double jnt_pos[OSC_KIN_MAX_BODIES][3];           /* jnt_pos   (body frame; hinge/ball anchor)*/
   double armature[OSC_KIN_MAX_BODIES];             /* dof_armature of every dof of the joint   */
   double mass[OSC_KIN_MAX_BODIES];                 /* body_mass                                */
   double ipos[OSC_KIN_MAX_BODIES][3];              /* body_ipos (COM, body frame)              */

@@ -75,7 +75,6 @@ struct DevParams {
   // wheel no-slip rows (models built with them only; walter_sr_wheels/autogen/autogen.py:128-240)
   int32_t wheel_dof[OSC_MAX_SITES];  // dof of wheel i's joint, -1 = no rolling term
   double wheel_radius[OSC_MAX_SITES];
-  double wheel_penalty;              // equality-row penalty D_w, x max diag(Hr)
   double wheel_tol;                  // interior point: |row residual| <= wheel_tol to stop
   double refine_max_move;            // a refinement moving y by more (relative) is rejected
   int32_t refine_dual_extra;         // WH with duals requested: this many more refinement steps
@@ -126,13 +125,19 @@ struct Dims {
   // interior-point result handed to the refinement kernel (and, with duals requested, to the
   // dual kernel): [y | q (lambda on rows with lambda > s, else 0; row slots) | status]
   static constexpr int W_SOL = W_GD + even(NV);
-  // wheel rows: their multipliers nu (dual hand-off), the rows in reduced coordinates
-  // A~ = E [X | x0] - [0 | e] with A~ [y; 1] = E dv - e, each row scaled to unit norm (NW x NY1P),
-  // and [D_w, pad, scale s_w (NW)]
+  // wheel rows: the multipliers w = L'nu_Q handed to the dual kernel; the rows in
+  // reduced coordinates [Q | q1] (orthonormal, NW x NY1P; Q y + q1 = 0 <=> E dv = e); the
+  // dv-space basis V = R E of E's row space, R, and the y-space transform L (Q = L V X)
   static constexpr int W_NU = W_SOL + even(NY) + NRL * 16 + 2;
   static constexpr int W_AW = W_NU + even(NW);
-  static constexpr int W_DW = W_AW + NW * NY1P;
-  static constexpr int WS = WH ? W_DW + 2 + even(NW) : W_NU;
+  static constexpr int W_WV = W_AW + NW * NY1P;
+  static constexpr int W_WR = W_WV + NW * NV;
+  static constexpr int W_WL = W_WR + NW * NW;
+  // the rotation: T (NY x NY, T[i][k] at i * NY + k) and per column k the Q row it carries (-1:
+  // a free direction)
+  static constexpr int W_T = W_WL + NW * NW;
+  static constexpr int W_PIN = W_T + NY * NY;
+  static constexpr int WS = WH ? W_PIN + even(NY) : W_NU;
   // ---- warm state per env (doubles): [valid flag, pad | y (NY, padded) | lambda (row slots)] ----
   static constexpr int WW_Y = 2;
   static constexpr int WW_L = WW_Y + even(NY);
@@ -157,9 +162,16 @@ struct Dims {
   static constexpr int O_HA = R1 + R2;
   static constexpr int O_X = O_HA + even(NA * NA);
   static constexpr int O_MASK = O_X + NV * NY1P;
-  static constexpr int O_WE = O_MASK + even(NC);          // WH: E (NW x NV) | e (NW)
-  static constexpr int O_WA = O_WE + NW * NV + even(NW);  // WH: A~ (NW x NY1P)
-  static constexpr int SMEM = O_WA + NW * NY1P;
+  // WH: Gram-Schmidt row sets, one lane per column: [E | e | I] (dv space) and [V X | V x0 - vs
+  // | I] (y space); the identity columns accumulate the transforms R and L
+  static constexpr int WEST = even(NV + 1 + NW);
+  static constexpr int WAST = NY1P + NW;
+  static constexpr int O_WE = O_MASK + even(NC);
+  static constexpr int O_WA = O_WE + NW * WEST;
+  // WH: Gram-Schmidt of [Q; I_NY] (NW + NY rows of NY) -> the basis T of the y space whose first
+  // columns are Q's rows (compacted in place: row k = column k of T)
+  static constexpr int O_WT = O_WA + NW * WAST;
+  static constexpr int SMEM = O_WT + (WH ? (NW + NY) * NY : 0);
   static_assert(NW <= kRow, "IPM: one wheel row per lane of the env's row");
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");
@@ -467,6 +479,64 @@ __device__ __forceinline__ double bcast_guarded(double v) {
 // Dense products of the assembly (H_dv X, X'(H_dv X), and 2 A'WA where it fits one tile) on the
 // FP64 matrix cores (v_mfma_f64_16x16x4f64).
 typedef double d4 __attribute__((ext_vector_type(4)));
+
+// Sum over the 64 lanes, the same value on every lane (lane 0's butterfly result broadcast).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return __shfl(v, 0, kWave);
+}
+
+// Modified Gram-Schmidt over the NR rows of an LDS row set (row stride `stride`, `ncol` columns,
+// one lane per column): the first NDOT columns are made orthonormal, the other columns follow the
+// same row operations (a right-hand side, identity columns accumulating the transform).  A row
+// whose residual is not above `drop` x its original norm is dependent on the earlier ones and
+// becomes zero (with its transform row).  Every decision is wave-uniform.
+template <int NR, int NDOT>
+__device__ __forceinline__ void wave_mgs(double* rows, int stride, int ncol, int lane,
+                                         double drop) {
+  double a[NR];
+  const bool cv = lane < ncol;
+#pragma unroll
+  for (int w = 0; w < NR; ++w) a[w] = cv ? rows[w * stride + lane] : 0.0;
+  const bool dv = lane < NDOT;
+#pragma unroll
+  for (int w = 0; w < NR; ++w) {
+    const double n0 = sqrt(wave_sum(dv ? a[w] * a[w] : 0.0));
+#pragma unroll
+    for (int v = 0; v < w; ++v) {
+      const double cf = wave_sum(dv ? a[v] * a[w] : 0.0);
+      a[w] = fma(-cf, a[v], a[w]);
+    }
+    const double nn = sqrt(wave_sum(dv ? a[w] * a[w] : 0.0));
+    const double sc = (nn > drop * n0 && nn > 0.0) ? 1.0 / nn : 0.0;
+    a[w] *= sc;
+  }
+  if (cv) {
+#pragma unroll
+    for (int w = 0; w < NR; ++w) rows[w * stride + lane] = a[w];
+  }
+}
+
+// The same over rows held in LDS (loops not unrolled: for long row sets).
+__device__ __noinline__ void wave_mgs_lds(double* rows, int nrows, int stride, int ncol, int ndot,
+                                          int lane, double drop) {
+  const bool cv = lane < ncol, dv = lane < ndot;
+  for (int w = 0; w < nrows; ++w) {
+    double aw = cv ? rows[w * stride + lane] : 0.0;
+    const double n0 = sqrt(wave_sum(dv ? aw * aw : 0.0));
+    for (int v = 0; v < w; ++v) {
+      const double av = cv ? rows[v * stride + lane] : 0.0;
+      const double cf = wave_sum(dv ? av * aw : 0.0);
+      aw = fma(-cf, av, aw);
+    }
+    const double nn = sqrt(wave_sum(dv ? aw * aw : 0.0));
+    const double sc = (nn > drop * n0 && nn > 0.0) ? 1.0 / nn : 0.0;
+    if (cv) rows[w * stride + lane] = aw * sc;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
 
 // The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
 // of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
@@ -835,6 +905,140 @@ __device__ __forceinline__ void setup_env(
     STAMP_END(8);
     STAMP_BEGIN();
   }
+  if constexpr (D::WH) {
+    // ---- wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240) ----
+    // E dv = e with, for contact wheel i (mask m_i), rows 2i (longitudinal) and 2i + 1 (lateral):
+    //   m_i (d_roll' J_p,i - r_i e_k') dv = -m_i d_roll' b_i,   m_i d_lat' J_p,i dv = -m_i d_lat' b_i
+    // (J_p,i, b_i: the contact site's translational rows of J and b).  Seven or eight grounded
+    // wheels give 14-16 rows on nv = 14 accelerations: dependent, and in y = (u, z) coordinates
+    // (dv = X [y; 1]) badly scaled.  So:
+    //   1. V = R E: an orthonormal basis of E's row space (Gram-Schmidt, dependent rows dropped);
+    //      V dv = vs (vs = R e) is the same constraint set.
+    //   2. X <- (I - V'V) X + V'[0 | vs]: the accelerations' components along the constrained
+    //      directions are replaced by their constrained values.  On the feasible set this is the
+    //      same dv, so the QP's optimum is unchanged, but Hr = X'H_dv X loses the large curvature
+    //      (and the gradient its large terms) in exactly the directions the rows fix -- with all
+    //      rows independent of rank nv, X's y columns are exactly zero.
+    //   3. [Q | q1] = L [V X | V x0 - vs]: the rows in y coordinates, orthonormalised.  The
+    //      interior point and the refinement carry them as exact equality rows.
+    static_assert(D::JG && D::NW <= kRow, "wheel rows: contact rows of J staged in LDS");
+    constexpr int NW = D::NW, WEST = D::WEST, WAST = D::WAST;
+    double* sWE = sm + D::O_WE;
+    double* sWA = sm + D::O_WA;
+    const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
+    for (int p = lane; p < NW * WEST; p += kWave) {
+      const int w = p / WEST, c = p % WEST;
+      const int i = w >> 1, side = w & 1;
+      double acc = 0.0;
+      if (c <= NV) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const double dc = wd[i * 6 + side * 3 + q];
+          const double v = (c == NV) ? gb[static_cast<size_t>(env) * S + JC0 + 3 * i + q]
+                                     : sA[(3 * i + q) * NAP + c];   // contact row 3 i + q of J
+          acc = fma(dc, v, acc);
+        }
+        if (c < NV && side == 0 && c == P->wheel_dof[i]) acc -= P->wheel_radius[i];
+        acc *= (c == NV) ? -sMask[i] : sMask[i];
+      } else {
+        acc = (c - NV - 1 == w) ? 1.0 : 0.0;   // R accumulates here
+      }
+      sWE[p] = acc;
+    }
+    wave_sync();
+    wave_mgs<NW, NV>(sWE, WEST, NV + 1 + NW, lane, 1e-9);   // rows [V | vs | R]
+    wave_sync();
+    int rank = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) rank += (sWE[w * WEST + w + NV + 1] != 0.0) ? 1 : 0;
+    // P = V X - [0 | vs] and the identity columns of L
+    for (int p = lane; p < NW * WAST; p += kWave) {
+      const int w = p / WAST, c = p % WAST;
+      double acc;
+      if (c < NY1P) {
+        acc = (c == NY) ? -sWE[w * WEST + NV] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) acc = fma(sWE[w * WEST + j], sX[j * NY1P + c], acc);
+      } else {
+        acc = (c - NY1P == w) ? 1.0 : 0.0;
+      }
+      sWA[p] = acc;
+    }
+    wave_sync();
+    // X <- X - V'P (rank nv: the y columns are the constrained accelerations' -- exactly zero)
+    double* const wx = ws + static_cast<size_t>(env) * D::WS + D::W_X;
+    for (int p = lane; p < NV * NY1P; p += kWave) {
+      const int j = p / NY1P, c = p % NY1P;
+      double v = sX[p];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v = fma(-sWE[w * WEST + j], sWA[w * WAST + c], v);
+      v = (rank == NV && c < NY) ? 0.0 : v;
+      sX[p] = v;
+      wx[p] = v;
+    }
+    wave_sync();
+    wave_mgs<NW, NY>(sWA, WAST, WAST, lane, 1e-9);   // rows [Q | q1 | 0 | L]
+    wave_sync();
+    double* const wsw = ws + static_cast<size_t>(env) * D::WS;
+    for (int p = lane; p < NW * NY1P; p += kWave)
+      wsw[D::W_AW + p] = sWA[(p / NY1P) * WAST + p % NY1P];
+    for (int p = lane; p < NW * NV; p += kWave) wsw[D::W_WV + p] = sWE[(p / NV) * WEST + p % NV];
+    for (int p = lane; p < NW * NW; p += kWave) {
+      const int w = p / NW, c = p % NW;
+      wsw[D::W_WR + p] = sWE[w * WEST + NV + 1 + c];
+      wsw[D::W_WL + p] = sWA[w * WAST + NY1P + c];
+    }
+    // 4. T: an orthonormal basis of the y space whose first r' columns are Q's (nonzero) rows and
+    //    the rest span their null space (Gram-Schmidt of [Q; I]).  The interior point and the
+    //    refinement solve their Newton systems in y^ = T'y with the rows' coordinates pinned:
+    //    the rows hold exactly, and nothing of the Hessian's curvature along them enters the
+    //    factorisation.  X^ = X'T replaces X, so [Hr | g] below come out in these
+    //    coordinates.
+    double* sWT = sm + D::O_WT;
+    for (int p = lane; p < (NW + NY) * NY; p += kWave) {
+      const int w = p / NY, c = p % NY;
+      sWT[p] = (w < NW) ? sWA[w * WAST + c] : ((c == w - NW) ? 1.0 : 0.0);
+    }
+    wave_sync();
+    wave_mgs_lds(sWT, NW + NY, NY, NY, NY, lane, 1e-9);
+    wave_sync();
+    int kept = 0;
+    for (int w = 0; w < NW + NY; ++w) {
+      const double a = lane < NY ? sWT[w * NY + lane] : 0.0;
+      if (wave_sum(a * a) > 0.0) {   // wave-uniform
+        if (kept < NY) {
+          if (lane < NY) sWT[kept * NY + lane] = a;   // in place: kept <= w
+          if (lane == 0) wsw[D::W_PIN + kept] = (w < NW) ? static_cast<double>(w) : -1.0;
+        }
+        ++kept;
+      }
+      wave_sync();
+    }
+    for (int k = kept; k < NY; ++k) {   // (never in practice: a column short -> pinned at zero)
+      if (lane < NY) sWT[k * NY + lane] = 0.0;
+      if (lane == 0) wsw[D::W_PIN + k] = -2.0;
+    }
+    wave_sync();
+    for (int p = lane; p < NY * NY; p += kWave) {
+      const int i = p / NY, k = p % NY;
+      wsw[D::W_T + p] = sWT[k * NY + i];   // T[i][k]
+    }
+    // X^ = X'T (y columns; the affine column stays), staged in sWE (free now)
+    for (int p = lane; p < NV * NY; p += kWave) {
+      const int j = p / NY, k = p % NY;
+      double v = 0.0;
+#pragma unroll 8
+      for (int i = 0; i < NY; ++i) v = fma(sX[j * NY1P + i], sWT[k * NY + i], v);
+      sWE[p] = v;
+    }
+    wave_sync();
+    for (int p = lane; p < NV * NY; p += kWave) {
+      const int j = p / NY, k = p % NY;
+      sX[j * NY1P + k] = sWE[p];
+      wx[j * NY1P + k] = sWE[p];
+    }
+    wave_sync();
+  }
   // J, M, C dead from here on (R1, R2 get reused)
 
   STAMP_END(2);
@@ -903,99 +1107,6 @@ __device__ __forceinline__ void setup_env(
           hacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xf[q][ab], t1[q / 4][bb][q % 4], hacc[t],
                                                          0, 0, 0);
     }
-    if constexpr (D::WH) {
-      // ---- wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240) ----
-      // E dv = e with, for contact wheel i (mask m_i), rows 2i (longitudinal) and 2i + 1 (lateral):
-      //   m_i (d_roll' J_p,i - r_i e_k') dv = -m_i d_roll' b_i,   m_i d_lat' J_p,i dv = -m_i d_lat' b_i
-      // (J_p,i, b_i: the contact site's translational rows of J and b).  In reduced coordinates
-      // A~ [y; 1] = E (X y + x0) - e, i.e. A~ = E [X | x0] - [0 | e], each row scaled to unit norm.
-      // They enter the reduced QP as the penalty D_w A~'A~ on [Hr | g]; the interior point and the
-      // refinement carry their multipliers (proximal method of multipliers).
-      static_assert(D::JG && D::NW % 4 == 0, "wheel rows: contact rows of J staged in LDS");
-      constexpr int NW = D::NW;
-      double* sE = sm + D::O_WE;   // E (NW x NV) | e (NW); later the row scales
-      double* sAw = sm + D::O_WA;  // A~ (NW x NY1P)
-      const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
-      for (int p = lane; p < NW * NV + NW; p += kWave) {
-        const bool rhs = p >= NW * NV;
-        const int w = rhs ? p - NW * NV : p / NV, j = rhs ? 0 : p % NV;
-        const int i = w >> 1, side = w & 1;
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const double dc = wd[i * 6 + side * 3 + c];
-          const double v = rhs ? gb[static_cast<size_t>(env) * S + JC0 + 3 * i + c]
-                               : sA[(3 * i + c) * NAP + j];   // contact row 3 i + c of J
-          acc = fma(dc, v, acc);
-        }
-        if (!rhs && side == 0 && j == P->wheel_dof[i]) acc -= P->wheel_radius[i];
-        const double m = sMask[i];
-        sE[p] = rhs ? -(m * acc) : m * acc;
-      }
-      wave_sync();
-      for (int p = lane; p < NW * NY1P; p += kWave) {
-        const int w = p / NY1P, c = p % NY1P;
-        double acc = (c == NY) ? -sE[NW * NV + w] : 0.0;
-#pragma unroll
-        for (int j = 0; j < NV; ++j) acc = fma(sE[w * NV + j], sX[j * NY1P + c], acc);
-        sAw[p] = acc;   // (X's pad column is 0)
-      }
-      wave_sync();
-      double sc = 0.0;   // 1 / |A~_w| over the y columns (0: a zero row, a wheel off the ground)
-      if (lane < NW) {
-        double nn = 0.0;
-        for (int c = 0; c < NY; ++c) nn = fma(sAw[lane * NY1P + c], sAw[lane * NY1P + c], nn);
-        sc = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
-        sE[lane] = sc;
-      }
-      wave_sync();
-      for (int p = lane; p < NW * NY1P; p += kWave) sAw[p] *= sE[p / NY1P];
-      wave_sync();
-      // D_w = wheel_penalty x the largest diagonal entry of Hr as stored (the refinement's scale)
-      double dmax = 0.0;
-      {
-        int t = 0;
-#pragma unroll
-        for (int ab = 0; ab < CB; ++ab)
-#pragma unroll
-          for (int bb = ab; bb < CB; ++bb, ++t)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const int a = 16 * ab + lg + 4 * rr, b = 16 * bb + lc;
-              const int kz = (a >= NU) ? (a - NU) / 3 : 0;
-              const double mk = sMask[kz < NC ? kz : NC - 1];
-              double v = hacc[t][rr] + ((a < NU) ? wu2 : wr2);
-              v = (a >= NU && mk == 0.0) ? 1.0 : v;
-              dmax = (a == b && a < NY) ? fmax(dmax, fabs(v)) : dmax;
-            }
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, kWave));
-      const double dw = P->wheel_penalty * dmax;
-      // [Hr | g] += D_w A~'A~ on the FP64 matrix cores (K = the NW rows, four per step)
-#pragma unroll
-      for (int q = 0; q < NW / 4; ++q) {
-        double af[CB];
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          const int col = 16 * cb + lc;
-          const double v = sAw[(4 * q + lg) * NY1P + (col < NY1P ? col : 0)];
-          af[cb] = col < NY1P ? v : 0.0;
-        }
-        int t = 0;
-#pragma unroll
-        for (int ab = 0; ab < CB; ++ab)
-#pragma unroll
-          for (int bb = ab; bb < CB; ++bb, ++t)
-            hacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(dw * af[ab], af[bb], hacc[t], 0, 0, 0);
-      }
-      for (int p = lane; p < NW * NY1P; p += kWave) wsv[D::W_AW + p] = sAw[p];
-      if (lane == 0) {
-        wsv[D::W_DW] = dw;
-        wsv[D::W_DW + 1] = 0.0;
-      }
-      if (lane < NW) wsv[D::W_DW + 2 + lane] = sc;
-    }
     int tt = 0;
 #pragma unroll
     for (int ab = 0; ab < CB; ++ab)
@@ -1009,7 +1120,21 @@ __device__ __forceinline__ void setup_env(
           const double mk = sMask[kz < NC ? kz : NC - 1];
           double v = h[rr];
           if (a <= b && b < NY1 && !(a == NY && b == NY)) {
-            if (b < NY) {
+            if (b < NY && D::WH) {
+              // rotated coordinates: + T'WT, W = 2 (w_tau + w_reg) on u, 2 w_reg on z, 1 on a
+              // masked contact's (pinned) z -- whose coordinate T keeps as a unit vector
+              const double* sT = sm + D::O_WT;
+              double wab = 0.0;
+#pragma unroll 8
+              for (int i = 0; i < NY; ++i) {
+                const int ki = (i >= NU) ? (i - NU) / 3 : 0;
+                const double wi = (i < NU) ? wu2 : (sMask[ki] == 0.0 ? 1.0 : wr2);
+                wab = fma(wi * sT[a * NY + i], sT[b * NY + i], wab);
+              }
+              v += wab;
+              wsv[D::W_HR + a * NY + b] = v;
+              wsv[D::W_HR + b * NY + a] = v;
+            } else if (b < NY) {
               if (a == b && a < NU) v += wu2;
               if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
               wsv[D::W_HR + a * NY + b] = v;
@@ -1149,10 +1274,11 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
 // it at its own pivot step and may take garbage afterwards.
 //   forward   z = L^-1 r             a_j += (-z_k / D_k) * (L[j][k] D_k)
 //   backward  in D-scaled form       a_j = z_j - sum_{k>j} (L[k][j] D_j) x_k,  x_j = a_j / D_j
+// (ldl_fwd_rows / ldl_bwd_rows: the two halves, for callers that act on z in between.)
 template <int N>
-__device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const double (&c1)[N],
-                                               double dinv0, double dinv1,
-                                               double& a0, double& a1, int l) {
+__device__ __forceinline__ void ldl_fwd_rows(const double (&c0)[N], const double (&c1)[N],
+                                             double dinv0, double dinv1,
+                                             double& a0, double& a1, int l) {
   double z0 = 0.0, z1 = 0.0;                // z_j, saved at step j
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -1171,6 +1297,11 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   });
   a0 = z0;
   a1 = z1;
+}
+template <int N>
+__device__ __forceinline__ void ldl_bwd_rows(const double (&c0)[N], const double (&c1)[N],
+                                             double dinv0, double dinv1,
+                                             double& a0, double& a1, int l) {
   double x0 = 0.0, x1 = 0.0;
   static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
@@ -1189,6 +1320,13 @@ __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const doub
   });
   a0 = -x0;
   a1 = -x1;
+}
+template <int N>
+__device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const double (&c1)[N],
+                                               double dinv0, double dinv1,
+                                               double& a0, double& a1, int l) {
+  ldl_fwd_rows<N>(c0, c1, dinv0, dinv1, a0, a1, l);
+  ldl_bwd_rows<N>(c0, c1, dinv0, dinv1, a0, a1, l);
 }
 
 // WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
@@ -1219,9 +1357,22 @@ constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's itera
 // LDS doubles per env beyond the interior point's layout: the refinement's [X | H_dv | f_dv]
 // block, except that a fused pass with Hr in LDS moves X into Hr's region once the first K_A is
 // assembled (registers hold it from then on) and only keeps [H_dv | f_dv] apart.
+// WH: the wheel rows' LDS block of an env: the rotation T (T[i][k] at i * TST + k; odd stride:
+// lanes reading a row of T or a column hit distinct banks), the Q row each column of T carries
+// (-1: free), q1 per Q row, a staging vector for the rotations, and the rows' multipliers.
+template <class D>
+struct WheelLds {
+  static constexpr int NW = D::NW, NY = D::NY, TST = NY + 1;
+  static constexpr int T = 0;
+  static constexpr int PIN = even(NY * TST);
+  static constexpr int Q1 = PIN + even(NY);
+  static constexpr int ROT = Q1 + even(NW);
+  static constexpr int NUV = ROT + even(NY);
+  static constexpr int SIZE = NUV + even(NW);
+};
 template <class D, bool SMALL, int RF>
 constexpr int refine_lds_extra() {
-  if constexpr (D::WH && RF == kRfFused) return even(D::NW * D::NY1P);   // A~ (reads [X | ..] from L2)
+  if constexpr (D::WH && RF == kRfFused) return WheelLds<D>::SIZE;   // (reads [X | ..] from L2)
   else if constexpr (RF == kRfNone) return 0;
   else if constexpr (RF == kRfFused && !SMALL) return 0;   // reads [X | H_dv | f_dv] from L2
   else if constexpr (RF == kRfFused && ipm_hrl<D, SMALL, RF>())   // (DMA: whole 1 KB rows)
@@ -1284,7 +1435,13 @@ __device__ __forceinline__ void ipm_block(
   // (the pointers are formed after the interior-point loop: nothing extra lives across it)
   // (so does a model with wheel rows: its LDS block holds the rows A~ instead)
   constexpr bool kRefG = RF == kRfFused && (!SMALL || D::WH);
-  double* sAw = B + LY::IL;   // WH: A~ (NW x NY1P), row w read by lane w
+  constexpr bool WHR = D::WH && RF == kRfFused;   // the wheel rows' rotated Newton systems
+  using WL = WheelLds<D>;
+  double* sWT = B + LY::IL + WL::T;
+  double* sWPin = B + LY::IL + WL::PIN;
+  double* sWQ1 = B + LY::IL + WL::Q1;
+  double* sWRot = B + LY::IL + WL::ROT;
+  double* sWNu = B + LY::IL + WL::NUV;
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
@@ -1318,11 +1475,15 @@ __device__ __forceinline__ void ipm_block(
       bx.load(ws + static_cast<size_t>(env) * D::WS + D::W_X, l);
       bx.store(sRX, l);
     }
-    if constexpr (D::WH && RF == kRfFused) {
-      static_assert(D::W_AW % 2 == 0 && (D::NW * NY1P) % 2 == 0, "16-byte staging");
-      Batch2<D::NW * NY1P / 2, kRow> ba;
-      ba.load(ws + static_cast<size_t>(env) * D::WS + D::W_AW, l);
-      ba.store(sAw, l);
+    if constexpr (WHR) {   // T, the pin map, q1
+      const double* we = ws + static_cast<size_t>(env) * D::WS;
+#pragma unroll 8
+      for (int p = l; p < NY * NY; p += kRow) sWT[(p / NY) * WL::TST + p % NY] = we[D::W_T + p];
+      for (int p = l; p < NY; p += kRow) sWPin[p] = we[D::W_PIN + p];
+      if (l < D::NW) {
+        sWQ1[l] = we[D::W_AW + l * NY1P + NY];
+        sWNu[l] = 0.0;
+      }
     }
     bs.store(B, l);
     if (l < NC) sMask[l] = mk;
@@ -1459,33 +1620,109 @@ __device__ __forceinline__ void ipm_block(
     v2 = (jc == 0) ? b02 : (jc == 1) ? b12 : b22;
   };
 
-  // Wheel no-slip rows (WH): A~ [y; 1] = 0, each row w = lane w of the env's row.  The reduced
-  // Hessian / gradient already carry the penalty D_w A~'A~ (setup); the interior point adds
-  // A~' c for the multiplier centre c and moves c by D_w A~ [y; 1] after every step (proximal
-  // method of multipliers).
+  // Wheel no-slip rows (WH): Q [y; 1] = 0, orthonormal rows (setup_env).  The Newton systems of
+  // the interior point and the refinement are solved in y^ = T'y, T = [rows of Q | null-space
+  // basis] (setup_env): K^ = H^ + sum_r D_r (T'g_r)(T'g_r)' assembled from the rows g_r of G one
+  // original coordinate at a time (no cancellation of large entries), the coordinates along Q's
+  // rows pinned (identity rows, step = -(Q y + q1): the rows hold after every step).  The
+  // iterate itself stays in y coordinates.  (An earlier Schur-complement treatment of the rows on
+  // K's factor lost the Newton steps' accuracy next to nearly dependent active rows: DESIGN.md §3.)
   constexpr int NW = D::NW;
-  auto aw_rows = [&](const double* v) -> double {   // (A~ [v; 1])_l on lane l < NW, else 0
-    const double* a = sAw + (l < NW ? l : 0) * NY1P;
-    double acc = a[NY];
-#pragma unroll
-    for (int i = 0; i < NY; ++i) acc = fma(a[i], v[i], acc);
-    return l < NW ? acc : 0.0;
+  // this lane's slots: pinned?  (the Q row's q1 for the residual)
+  bool pin0 = false, pin1 = false;
+  double q10 = 0.0, q11 = 0.0;
+  auto rot_load_pins = [&]() {
+    if constexpr (WHR) {
+      const double p0v = sWPin[j0], p1v = sWPin[jj1];
+      pin0 = p0v != -1.0;
+      pin1 = v1 && p1v != -1.0;
+      q10 = p0v >= 0.0 ? sWQ1[static_cast<int>(p0v)] : 0.0;
+      q11 = (v1 && p1v >= 0.0) ? sWQ1[static_cast<int>(p1v)] : 0.0;
+    }
   };
-  auto aw_cols = [&](double v, double& o0, double& o1) {   // (A~' v) at the lane's slots j0, jj1
+  // T'v and T v for a y-space vector held in the lane slots (staged through sWRot)
+  auto rot_in = [&](double v0, double v1v, double& o0, double& o1) {
+    wave_sync();
+    sWRot[j0] = v0;
+    if (v1) sWRot[j1] = v1v;
+    wave_sync();
     double a0 = 0.0, a1 = 0.0;
-    static_for<0, NW>([&](auto W) {
-      constexpr int w = decltype(W)::value;
-      fmac_bcast2<w, w == 0>(a0, a1, v, sAw[w * NY1P + j0], sAw[w * NY1P + jj1]);
-    });
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      const double r = sWRot[i];
+      a0 = fma(sWT[i * WL::TST + j0], r, a0);
+      a1 = fma(sWT[i * WL::TST + jj1], r, a1);
+    }
     o0 = a0;
     o1 = a1;
+    wave_sync();
   };
-  double cw = 0.0, wnu0 = 0.0, wnu1 = 0.0, rwmax = 0.0, dw = 0.0;
-  if constexpr (D::WH && RF == kRfFused)
-    dw = ws[static_cast<size_t>(env) * D::WS + D::W_DW];
+  auto rot_out = [&](double v0, double v1v, double& o0, double& o1) {
+    wave_sync();
+    sWRot[j0] = v0;
+    if (v1) sWRot[j1] = v1v;
+    wave_sync();
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const double r = sWRot[k];
+      a0 = fma(sWT[j0 * WL::TST + k], r, a0);
+      a1 = fma(sWT[jj1 * WL::TST + k], r, a1);
+    }
+    o0 = a0;
+    o1 = a1;
+    wave_sync();
+  };
+  // rq: the rows' residual at the current y, on the pinned slots (q1 at the start, y = 0)
+  double rq0 = 0.0, rq1 = 0.0, rwmax = 0.0;
+  rot_load_pins();
+  rq0 = pin0 ? q10 : 0.0;
+  rq1 = pin1 ? q11 : 0.0;
 
   double c0[NY], c1[NY];
   double dinv0, dinv1;
+  // WH: c0 / c1 hold H^'s columns j0, jj1; add T'(G'DG)T from sDr (D per row slot) one original
+  // coordinate i at a time -- column j gains coef_i(j) T[i][:], coef_i(j) = (G'DG)[i][:] T[:][j]
+  // (torque rows: diagonal; a contact's rows: its 3 x 3 block) -- then pin Q's coordinates.
+  // Returns the assembled diagonal entries (the pivot threshold's reference).
+  auto assemble_rot = [&](double& dg0r, double& dg1r) {
+    if constexpr (WHR) {
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        double a0, a1;
+        if (i < NU) {
+          const double d = sDr[2 * i] + sDr[2 * i + 1];
+          a0 = d * sWT[i * WL::TST + j0];
+          a1 = d * sWT[i * WL::TST + jj1];
+        } else {
+          const int k = (i - NU) / 3, ci = (i - NU) % 3, zb = NU + 3 * k;
+          double b0, b1, b2;   // row ci of contact k's block (symmetric: its column ci)
+          contact_col(k, ci, b0, b1, b2);
+          a0 = b0 * sWT[zb * WL::TST + j0] + b1 * sWT[(zb + 1) * WL::TST + j0] +
+               b2 * sWT[(zb + 2) * WL::TST + j0];
+          a1 = b0 * sWT[zb * WL::TST + jj1] + b1 * sWT[(zb + 1) * WL::TST + jj1] +
+               b2 * sWT[(zb + 2) * WL::TST + jj1];
+        }
+#pragma unroll
+        for (int m = 0; m < NY; ++m) {
+          const double t = sWT[i * WL::TST + m];
+          c0[m] = fma(a0, t, c0[m]);
+          c1[m] = fma(a1, t, c1[m]);
+        }
+      }
+      double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+      for (int m = 0; m < NY; ++m) {
+        const bool pm = sWPin[m] != -1.0;
+        c0[m] = pin0 ? ((m == j0) ? 1.0 : 0.0) : (pm ? 0.0 : c0[m]);
+        c1[m] = pin1 ? ((m == jj1) ? 1.0 : 0.0) : (pm ? 0.0 : c1[m]);
+        d0 = (m == j0) ? c0[m] : d0;
+        d1 = (m == jj1) ? c1[m] : d1;
+      }
+      dg0r = d0;
+      dg1r = d1;
+    }
+  };
   // One-wave variant whose Hr does not fit the LDS (WaLTER: 32 x 32 x 4 envs): the lane's two Hr
   // columns are loaded once and kept in registers across the iterations (the one-wave kernel has
   // 512 of them, AGPRs included) instead of being re-read from L2 every iteration.
@@ -1711,18 +1948,25 @@ __device__ __forceinline__ void ipm_block(
     // ---- Newton matrix K = Hr + G' D G (columns j0, j1 in registers) and rd = Hr y + g + G'lam
     double rd0, rd1;
     GTw2(sVr, rd0, rd1);
+    if constexpr (WHR) rot_in(rd0, rd1, rd0, rd1);   // T'G'lam
     rd0 += g0;
     rd1 += g1;
-    if constexpr (D::WH) {   // + A~' c (the gradient of the augmented Lagrangian)
-      rd0 += wnu0;
-      rd1 += wnu1;
-    }
     double dg0 = hdg0, dg1 = hdg1;
-    if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);      // rd += Hr y (y broadcast by DPP)
+    if constexpr (WHR) {   // rd^ += H^ y^
+      if (!init) {
+        double yh0, yh1;
+        rot_in(y0, y1, yh0, yh1);
+        dot_rows<NY>(rd0, rd1, yh0, yh1, c0, c1);
+      }
+    } else {
+      if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);    // rd += Hr y (y broadcast by DPP)
+    }
     STAMP_END(8);
     STAMP_BEGIN();
     // G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
-    {
+    if constexpr (WHR) {
+      assemble_rot(dg0, dg1);
+    } else {
       static_assert(D::NU <= kRow, "torque variables in the first column slot");
       const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
       const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
@@ -1734,7 +1978,7 @@ __device__ __forceinline__ void ipm_block(
     }
     STAMP_END(9);
     STAMP_BEGIN();
-    if (jk0 >= 0) {
+    if (!WHR && jk0 >= 0) {
       double a, b, cc;
       contact_col(jk0, jc0, a, b, cc);
       dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
@@ -1744,7 +1988,7 @@ __device__ __forceinline__ void ipm_block(
         c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
       }
     }
-    if (jk1 >= 0) {
+    if (!WHR && jk1 >= 0) {
       double a, b, cc;
       contact_col(jk1, jc1, a, b, cc);
       dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
@@ -1777,11 +2021,18 @@ __device__ __forceinline__ void ipm_block(
       }
       wave_sync();
       GTw2(sVr, dy0, dy1);
-      dy0 -= rd0;
-      dy1 -= rd1;
+      if constexpr (WHR) {   // in y^: T'(G'w) - rd^, the pinned slots step to the rows
+        rot_in(dy0, dy1, dy0, dy1);
+        dy0 = pin0 ? -rq0 : dy0 - rd0;
+        dy1 = pin1 ? -rq1 : dy1 - rd1;
+      } else {
+        dy0 -= rd0;
+        dy1 -= rd1;
+      }
       STAMP_END(4);
       STAMP_BEGIN();
       ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, dy0, dy1, l);
+      if constexpr (WHR) rot_out(dy0, dy1, dy0, dy1);
       sVy2[j0] = dy0;
       if (v1) sVy2[j1] = dy1;
       wave_sync();
@@ -1813,6 +2064,17 @@ __device__ __forceinline__ void ipm_block(
         sig_mu = q * q * mu;   // sigma = (mu_aff/mu)^2: the cube jams on rare envs (tools/ipm_hard.py)
 #pragma unroll
         for (int t = 0; t < NRL; ++t) dsdl[t] = ds[t] * dl[t];
+        if constexpr (WHR) {
+          // late stall: once the active rows' barrier terms pass ~1e10 their dense rank-one terms
+          // in the rotated Newton matrix swamp its small curvature and the affine step collapses
+          // (tools/wheel_one.py traces).  The iterate is as good as it gets there: stop on it
+          // (no step) and let the refinement finish the solve.
+          if (!done && mu <= 1e-8 && step < 0.1 && rwmax <= P->wheel_tol) {
+            done = true;
+            st = OSC_SOLVE_OK;
+            it_done = it;
+          }
+        }
       }
       wave_sync();
       STAMP_END(6);
@@ -1864,13 +2126,12 @@ __device__ __forceinline__ void ipm_block(
     if (v1) sVy[j1] = y1;
     load_hr();   // next iteration's Hr columns (the factor in c0/c1 is dead now)
     wave_sync();
-    if constexpr (D::WH) {
-      // the wheel rows' residual at the new iterate moves the multiplier centre (a converged env's
-      // iterate no longer moves: its centre stays)
-      const double r = aw_rows(sVy);
-      cw = done ? cw : fma(dw, r, cw);
-      aw_cols(cw, wnu0, wnu1);
-      rwmax = row_max(fabs(r));
+    if constexpr (WHR) {   // the rows' residual at the new iterate (next step, stop test)
+      double yh0, yh1;
+      rot_in(y0, y1, yh0, yh1);
+      rq0 = pin0 ? yh0 + q10 : 0.0;
+      rq1 = pin1 ? yh1 + q11 : 0.0;
+      rwmax = row_max(fmax(fabs(rq0), fabs(rq1)));
     }
     STAMP_END(7);
   }
@@ -1908,10 +2169,21 @@ __device__ __forceinline__ void ipm_block(
   // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
   // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
   // every other multiplier from the design vector itself.
+  // (w = L' nu: the multipliers of the rows [V X | V x0 - vs] before their orthonormalisation,
+  // which the dual kernel maps back to E's rows; every lane of the env's row takes part)
   auto put_wheel_duals = [&](double nu) {
     if constexpr (D::WH) {
-      if (want_dual && write_out && l < NW)
-        const_cast<double*>(ws)[static_cast<size_t>(env) * D::WS + D::W_NU + l] = nu;
+      if (want_dual) {
+        const double* Lw = ws + static_cast<size_t>(env) * D::WS + D::W_WL;
+        const int lc = l < NW ? l : 0;
+        double acc = 0.0;
+        static_for<0, NW>([&](auto W) {
+          constexpr int w = decltype(W)::value;
+          acc = fma(Lw[w * NW + lc], bcast_guarded<w>(nu), acc);
+        });
+        if (write_out && l < NW)
+          const_cast<double*>(ws)[static_cast<size_t>(env) * D::WS + D::W_NU + l] = acc;
+      }
     }
   };
   // the duals ask the refinement for more steps (its multipliers converge more slowly than y)
@@ -1922,26 +2194,29 @@ __device__ __forceinline__ void ipm_block(
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
       const double ytol = 1e-9 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)));
       double Dr[NRL], mur[NRL];
+      // WH: a row whose slack is within 1e-6 of the bound is active too -- next to the rows'
+      // Schur solves the interior point's multipliers of a weakly active row can be off by orders
+      // of magnitude while y is right (numpy model: 11 of 512 tumbling refinements rejected -> 0)
+      const double stol = D::WH ? 1e-6 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0))) : -1.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
-        const bool a = act[t] && lam[t] > s[t];
+        const bool a = act[t] && (lam[t] > s[t] || s[t] <= stol);
         Dr[t] = a ? dpen : 0.0;
         mur[t] = a ? lam[t] : 0.0;
       }
       const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg;
       double ya0 = y0, ya1 = y1;
       bool viol_env = false;
-      // wheel rows: always active, penalty D_w (already in K_A through Hr), multipliers nur
-      double nur = cw;
       const double* wenv = ws + static_cast<size_t>(env) * D::WS;
       const double* rX = kRefG ? wenv + D::W_X : sRX;
       const double* rH = kRefG ? wenv + D::W_HD : sRH;
       const double* rG = kRefG ? wenv + D::W_GD : sRG;
       constexpr int kUr = kRefG ? 2 : 32;   // workspace reads: few in flight (registers)
+      double dlast = 0.0;   // WH: the last refinement step's size (its convergence test)
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
-      for (int round = 0; round < 3; ++round) {
+      for (int round = 0; round < (WHR ? 5 : 3); ++round) {
         STAMP_BEGIN();
 #ifdef OSC_STAMPS
         st_acc[10] += 1ull << 40;   // rounds, in the top bits of the assembly+LDL slot
@@ -1962,13 +2237,15 @@ __device__ __forceinline__ void ipm_block(
         for (int t = 0; t < NRL; ++t) sDr[l + kRow * t] = Dr[t];
         ya0 = y0;
         ya1 = y1;
-        nur = cw;
         sVy[j0] = y0;
         if (v1) sVy[j1] = y1;
         wave_sync();
         // K_A in c0 / c1 (they hold Hr's columns)
         double dg0 = hdg0, dg1 = hdg1;
-        {
+        if constexpr (WHR) {
+          wave_sync();
+          assemble_rot(dg0, dg1);
+        } else {
           const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
           const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
           dg0 += du;
@@ -1977,7 +2254,7 @@ __device__ __forceinline__ void ipm_block(
             c0[i] += keep_lanes<rows_mask(1u << i)>(du);
           });
         }
-        if (jk0 >= 0) {
+        if (!WHR && jk0 >= 0) {
           double a, b, cc;
           contact_col(jk0, jc0, a, b, cc);
           dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
@@ -1987,7 +2264,7 @@ __device__ __forceinline__ void ipm_block(
             c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
           }
         }
-        if (jk1 >= 0) {
+        if (!WHR && jk1 >= 0) {
           double a, b, cc;
           contact_col(jk1, jc1, a, b, cc);
           dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
@@ -2061,6 +2338,19 @@ __device__ __forceinline__ void ipm_block(
         STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
         for (int k = 0; k < refine_steps; ++k) {
+          // WH: X holds X^ = X'T, so dv = X^ [y^; 1] (y^ = T'y staged in sVy2, free until the step)
+          // and the rows' residual at y comes with y^
+          const double* yv = sVy;
+          if constexpr (WHR) {
+            double yh0, yh1;
+            rot_in(ya0, ya1, yh0, yh1);
+            rq0 = pin0 ? yh0 + q10 : 0.0;
+            rq1 = pin1 ? yh1 + q11 : 0.0;
+            sVy2[j0] = yh0;
+            if (v1) sVy2[j1] = yh1;
+            wave_sync();
+            yv = sVy2;
+          }
           // dv = X [y; 1] (rows l, l + 16) -> sXb
 #pragma unroll
           for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
@@ -2069,7 +2359,7 @@ __device__ __forceinline__ void ipm_block(
               const double* xr = rX + rr * NY1P;
               double a = xr[NY];
 #pragma unroll kUr
-              for (int i = 0; i < NY; ++i) a = fma(xr[i], sVy[i], a);
+              for (int i = 0; i < NY; ++i) a = fma(xr[i], yv[i], a);
               sXb[rr] = a;
             }
           }
@@ -2095,24 +2385,60 @@ __device__ __forceinline__ void ipm_block(
 #pragma unroll
           for (int t = 0; t < NRL; ++t) sVr[l + kRow * t] = mur[t];
           wave_sync();
+          if constexpr (D::WH && RF == kRfFused) {
+            // gx <- (I - V'V) gx: X's columns are orthogonal to V (setup_env), so this changes
+            // nothing in exact arithmetic, but it drops gx's large components along the rows'
+            // constrained directions before X' multiplies them (numpy model: 5e-9 -> 1.5e-9 worst)
+            const double* Vw = wenv + D::W_WV;
+            double vg = 0.0;
+            if (l < NW) {
+#pragma unroll
+              for (int j = 0; j < NV; ++j) vg = fma(Vw[l * NV + j], sDr[j], vg);
+            }
+            double corr[(NV + kRow - 1) / kRow];
+#pragma unroll
+            for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) corr[t] = 0.0;
+            static_for<0, NW>([&](auto W) {
+              constexpr int w = decltype(W)::value;
+              const double bw = bcast_guarded<w>(vg);
+#pragma unroll
+              for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
+                const int rr = l + kRow * t;
+                corr[t] = fma(Vw[w * NV + (rr < NV ? rr : 0)], bw, corr[t]);
+              }
+            });
+            wave_sync();
+#pragma unroll
+            for (int t = 0; t < (NV + kRow - 1) / kRow; ++t)
+              if (l + kRow * t < NV) sDr[l + kRow * t] -= corr[t];
+            wave_sync();
+          }
           // r_j = X[:, j]' gx + diag_j y_j + (G_A' mu)_j for the lane's two variables
+          // (WH, in y^: X^'gx + T'(W y + G_A' mu))
           double r0 = (j0 < NU ? wu : wz) * ya0, r1 = (jj1 < NU ? wu : wz) * ya1;
+          double gm0, gm1;
+          if constexpr (WHR) {
+            GTw2(sVr, gm0, gm1);
+            r0 += gm0;
+            r1 += gm1;
+            rot_in(r0, r1, r0, r1);
+          }
 #pragma unroll kUr
           for (int i = 0; i < NV; ++i) {
             r0 = fma(rX[i * NY1P + j0], sDr[i], r0);
             r1 = fma(rX[i * NY1P + jj1], sDr[i], r1);
           }
-          double gm0, gm1;
-          GTw2(sVr, gm0, gm1);
-          r0 += gm0;
-          r1 += gm1;
-          double rw = 0.0;   // WH: the wheel rows' residual A~ [y; 1] (lane w)
-          if constexpr (D::WH) {
-            double q0, q1;
-            aw_cols(nur, q0, q1);   // + A~' nu
-            r0 += q0;
-            r1 += q1;
-            rw = aw_rows(sVy);
+          if constexpr (!WHR) {   // (this order: the feature-off results stay bitwise)
+            GTw2(sVr, gm0, gm1);
+            r0 += gm0;
+            r1 += gm1;
+          }
+          if constexpr (WHR) {
+            // the pinned coordinates of r^ are Q (grad f + G_A' mu): their negatives are the rows'
+            // multipliers (least squares; the last step's stand)
+            const double p0v = sWPin[j0], p1v = sWPin[jj1];
+            if (p0v >= 0.0) sWNu[static_cast<int>(p0v)] = -r0;
+            if (v1 && p1v >= 0.0) sWNu[static_cast<int>(p1v)] = -r1;
           }
           wave_sync();
           double R3[NRL];
@@ -2124,14 +2450,17 @@ __device__ __forceinline__ void ipm_block(
           wave_sync();
           double b0, b1;
           GTw2(sVr, b0, b1);
-          if constexpr (D::WH) {   // + D_w A~' A~ [y; 1]
-            double e0, e1;
-            aw_cols(dw * rw, e0, e1);
-            b0 += e0;
-            b1 += e1;
-          }
+          if constexpr (WHR) rot_in(b0, b1, b0, b1);
           double d0 = -r0 - b0, d1 = -r1 - b1;
+          if constexpr (WHR) {
+            d0 = pin0 ? -rq0 : d0;
+            d1 = pin1 ? -rq1 : d1;
+          }
           ldl_solve_rows<NY>(c0, c1, dinv0, dinv1, d0, d1, l);
+          if constexpr (WHR) {
+            rot_out(d0, d1, d0, d1);
+            dlast = row_max(fmax(fabs(d0), v1 ? fabs(d1) : 0.0));
+          }
           sVy2[j0] = d0;
           if (v1) sVy2[j1] = d1;
           wave_sync();
@@ -2143,7 +2472,6 @@ __device__ __forceinline__ void ipm_block(
           sVy[j0] = ya0;
           if (v1) sVy[j1] = ya1;
           wave_sync();
-          if constexpr (D::WH) nur = fma(dw, aw_rows(sVy), nur);   // nu += D_w A~ [y + dy; 1]
         }
         // rows the refined point violates join the active set
         double nviol = 0.0;
@@ -2153,6 +2481,20 @@ __device__ __forceinline__ void ipm_block(
           Dr[t] = v ? dpen : Dr[t];
           nviol += v ? 1.0 : 0.0;
         }
+        if constexpr (WHR) {
+          // ... and (WH, whose slack-based active set can include a row the optimum leaves) rows
+          // whose multiplier came out negative leave it
+          double mmax = 0.0;
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) mmax = fmax(mmax, Dr[t] != 0.0 ? fabs(mur[t]) : 0.0);
+          const double mtol = 1e-9 * (1.0 + row_max(mmax));
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) {
+            const bool leave = Dr[t] != 0.0 && mur[t] < -mtol;
+            Dr[t] = leave ? 0.0 : Dr[t];
+            nviol += leave ? 1.0 : 0.0;
+          }
+        }
         viol_env = mine && row_max(nviol) > 0.0;
         STAMP_END(11);
         if (__ballot(viol_env) == 0) break;
@@ -2160,10 +2502,20 @@ __device__ __forceinline__ void ipm_block(
       // keep the refined iterate when it is feasible, finite and close to the interior point's
       const double mv = fmax(fabs(ya0 - y0), v1 ? fabs(ya1 - y1) : 0.0);
       const double my = fmax(fabs(y0), v1 ? fabs(y1) : 0.0);
+      // (WH: the interior point stops earlier (eps_mu 1e-9, osc_model_create: past that its
+      // rotated Newton systems lose accuracy), so the refinement may move y further; it is kept
+      // when it has converged -- its last step below 1e-10 of y -- within 0.1 of y)
       const double ok =
-          (isfinite(ya0) && isfinite(ya1) && mv <= P->refine_max_move * (1.0 + my)) ? 1.0 : 0.0;
-      // (WH: and the wheel rows hold at the refined point; sVy holds it)
-      const double wres = D::WH ? row_max(fabs(aw_rows(sVy))) : 0.0;
+          (isfinite(ya0) && isfinite(ya1) &&
+           (WHR ? (mv <= 0.1 * (1.0 + my) && dlast <= 1e-10 * (1.0 + my))
+                : mv <= P->refine_max_move * (1.0 + my))) ? 1.0 : 0.0;
+      // (WH: and the wheel rows hold at the refined point)
+      double wres = 0.0;
+      if constexpr (WHR) {
+        double yh0, yh1;
+        rot_in(ya0, ya1, yh0, yh1);
+        wres = row_max(fmax(pin0 ? fabs(yh0 + q10) : 0.0, pin1 ? fabs(yh1 + q11) : 0.0));
+      }
       const bool keep = !viol_env && row_min(ok) == 1.0 && wres <= ytol;
       if (mine && keep) {
         y0 = ya0;
@@ -2173,7 +2525,7 @@ __device__ __forceinline__ void ipm_block(
       // a converged env whose refinement is rejected keeps the interior point's iterate, and says
       // so: it is only as accurate as the interior point's stop
       if (mine && !keep) st = OSC_SOLVE_UNREFINED;
-      put_wheel_duals((mine && keep) ? nur : cw);
+      put_wheel_duals((mine && keep && l < NW) ? sWNu[l] : 0.0);
       wave_sync();
       sVy[j0] = y0;
       if (v1) sVy[j1] = y1;
@@ -2184,7 +2536,7 @@ __device__ __forceinline__ void ipm_block(
 #ifdef OSC_STAMPS
   if constexpr (RF == kRfFused) STAMP_STORE();
 #endif
-  if (!refined) put_wheel_duals(cw);
+  if (!refined) put_wheel_duals(0.0);
   // ---------------- outputs: tau = y_u;  x = (dv, u, z) with dv = X [y; 1] -----------------
   if (REFINE && !refined) {   // the interior point kernel's outputs stand
     if (write_out && l == 0 && gstatus && st == OSC_SOLVE_UNREFINED) gstatus[env] = st;
@@ -2196,6 +2548,15 @@ __device__ __forceinline__ void ipm_block(
     if (write_out) gtau[static_cast<size_t>(env) * NU + l] = tq;
   }
   if (gx != nullptr) {   // dv = X [y; 1], two rows per lane
+    const double* yv = sVy;
+    if constexpr (WHR) {   // X^ = X'T: dv = X^ [T'y; 1]
+      double yh0, yh1;
+      rot_in(y0, y1, yh0, yh1);
+      sVy2[j0] = yh0;
+      if (v1) sVy2[j1] = yh1;
+      wave_sync();
+      yv = sVy2;
+    }
 #pragma unroll
     for (int t = 0; t < (NV + kRow - 1) / kRow; ++t) {
       const int rr = l + kRow * t;
@@ -2203,7 +2564,7 @@ __device__ __forceinline__ void ipm_block(
         const double* xr = ws + static_cast<size_t>(env) * D::WS + D::W_X + rr * NY1P;
         double xb = xr[NY];
 #pragma unroll
-        for (int i = 0; i < NY; ++i) xb = fma(xr[i], sVy[i], xb);
+        for (int i = 0; i < NY; ++i) xb = fma(xr[i], yv[i], xb);
         sXb[rr] = xb;
       }
     }
@@ -2247,8 +2608,11 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
     int flags) {
-  // one-wave variant: four workgroups per CU (160 KB of LDS), never five
-  static_assert(!SMALL || ipm_lds_doubles<D, SMALL, RF>() * 8 <= 160 * 1024 / 4, "IPM LDS");
+  // one-wave variant: four workgroups per CU (160 KB of LDS), never five.  (The opt-in wheel
+  // rows' Schur blocks take it to 53 KB per wave: three per CU)
+  static_assert(!SMALL || ipm_lds_doubles<D, SMALL, RF>() * 8 <= 160 * 1024 / (D::WH ? 3 : 4),
+                "IPM LDS");
+  static_assert(ipm_lds_doubles<D, SMALL, RF>() * 8 <= 64 * 1024, "IPM LDS per workgroup");
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, RF>()];
   ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                     gstatus, giters, gwarm, flags, sm);
@@ -2292,7 +2656,7 @@ __global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, Pair
 // sign convention (H x + f + A'y = 0, y >= 0 on an active upper bound, <= 0 on a lower one),
 // recovered from the returned design vector x = (dv, u, z) by stationarity:
 //   dynamics rows  nu = -M^-1 (H_dv dv + f_dv + E'nu_w)             (the dv block)
-//   wheel rows     nu_w: the refinement's multipliers (W_NU), unscaled s_w nu~_w
+//   wheel rows     nu_w = R'(w - V g0) from the refinement's multipliers w (W_NU)
 //   u box rows     nu_a - 2 (w_tau + w_reg) u                        (the u block)
 //   contact k      r_k = 2 w_reg z_k - Jc_k'nu must be balanced by its active rows: the pyramid
 //                  rows, fz >= 0, fz <= big_number (a tiny non-negative least squares over the
@@ -2324,11 +2688,31 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   const double* J = gJ + static_cast<size_t>(env) * S * NV;
   const double* mask = gmask + static_cast<size_t>(env) * NC;
   for (int p = lane; p < NV * NV; p += kWave) sL[p] = gM[static_cast<size_t>(env) * NV * NV + p];
-  if (lane < NW) snu[lane] = w[D::W_DW + 2 + lane] * w[D::W_NU + lane];
-  __syncthreads();
-  if (lane < NV) {   // g_x = H_dv dv + f_dv (+ E' nu_w)
+  if (lane < NV) {   // g0 = H_dv dv + f_dv
     double a = w[D::W_GD + lane];
     for (int j = 0; j < NV; ++j) a = fma(w[D::W_HD + lane * NV + j], x[j], a);
+    sg[lane] = a;
+  }
+  __syncthreads();
+  if constexpr (D::WH) {
+    // nu_w = R'(w - V g0): the interior point's rows were Q = L V X with V = R E (setup_env);
+    // stationarity X'(g0 + E'nu_w) = X'(g0 - V'V g0) + Q'nu_Q holds with E'nu_w = V'(L'nu_Q - V g0)
+    __shared__ double st[NW > 0 ? NW : 1];
+    if (lane < NW) {
+      double a = w[D::W_NU + lane];
+      for (int j = 0; j < NV; ++j) a = fma(-w[D::W_WV + lane * NV + j], sg[j], a);
+      st[lane] = a;
+    }
+    __syncthreads();
+    if (lane < NW) {
+      double a = 0.0;
+      for (int v = 0; v < NW; ++v) a = fma(w[D::W_WR + v * NW + lane], st[v], a);
+      snu[lane] = a;
+    }
+  }
+  __syncthreads();
+  if (lane < NV) {   // g_x = g0 (+ E' nu_w)
+    double a = sg[lane];
     if constexpr (D::WH) {
       const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
       for (int i = 0; i < NC; ++i) {
@@ -2595,7 +2979,8 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   // full-space refinement: two steps with one factorisation, penalty 1e2 x the
   // largest reduced-Hessian diagonal (numpy model: <= 3e-12 normwise on Go2 / WaLTER batches,
   // from up to 7e-6 without it)
-  hp.refine_steps = 2;
+  // (wheel rows: eight, run to convergence from the interior point's earlier stop)
+  hp.refine_steps = d.wheel_rows ? 8 : 2;
   hp.refine_penalty = 1e2;
   if (const char* e = std::getenv("OSC_REFINE_STEPS")) hp.refine_steps = std::atoi(e);
   if (const char* e = std::getenv("OSC_EPS_MU")) hp.eps_mu = std::atof(e);   // sweeps only
@@ -2611,16 +2996,14 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   // The YAML's Go2 stop (eps_mu 1e-9) presumes the refinement finishes the solve; without it the
   // interior point runs to 1e-12 itself.
   if (hp.refine_steps <= 0) hp.eps_mu = std::fmin(hp.eps_mu, 1e-12);
-  // wheel no-slip rows: penalty D_w = 1e3 x max diag(Hr) on the unit-norm rows,
-  // interior point stops once every row holds to 1e-8 (the refinement then solves them exactly)
+  // wheel no-slip rows: pinned coordinates of the interior point's Newton systems,
+  // so every step leaves them holding to rounding; the stop test asks 1e-6
   for (int i = 0; i < OSC_MAX_SITES; ++i) hp.wheel_dof[i] = -1;
   for (int i = 0; d.wheel_rows && i < d.nc; ++i) {
     hp.wheel_dof[i] = d.wheel_dof[i];
     hp.wheel_radius[i] = d.wheel_radius[i];
   }
-  hp.wheel_penalty = 1e3;
-  hp.wheel_tol = 1e-8;
-  if (const char* e = std::getenv("OSC_WHEEL_PENALTY")) hp.wheel_penalty = std::atof(e);
+  hp.wheel_tol = 1e-6;
   if (const char* e = std::getenv("OSC_WHEEL_TOL")) hp.wheel_tol = std::atof(e);
 
   osc_model* m = new (std::nothrow) osc_model;

@@ -62,7 +62,24 @@ def _constraints(qp: QPData):
             ineq.append((i, +1.0, hi))
         if lo > -INF_THRESH:
             ineq.append((i, -1.0, -lo))
-    return eq, ineq
+    return _independent(qp.A, eq), ineq
+
+
+def _independent(A, eq):
+    """A maximal linearly independent subset of the equality rows (QR with column pivoting of the
+    unit-scaled A_eq').  The wheel no-slip rows of seven or eight grounded wheels are 14-16 rows on
+    nv = 14 accelerations, so some are implied by the others (consistent by construction); kept,
+    they make every working-set KKT matrix singular.  The rows kept are the original ones (an
+    orthonormalised basis instead moves the constraint set by its rounding, amplified by the
+    rows' near-dependence)."""
+    if len(eq) == 0:
+        return eq
+    import scipy.linalg
+    rows = A[eq] / np.linalg.norm(A[eq], axis=1, keepdims=True)
+    _, R, piv = scipy.linalg.qr(rows.T, mode="economic", pivoting=True)
+    d = np.abs(np.diag(R))
+    rank = int((d > 1e-10 * d[0]).sum())
+    return sorted(eq[p] for p in piv[:rank])
 
 
 def _feasible_start(model: OSCModel, qp: QPData, M, C, J):
@@ -115,14 +132,18 @@ def kkt_certificate(qp: QPData, x: np.ndarray, y: np.ndarray) -> dict:
     bnd = np.where(hi_fin, np.abs(qp.u), 0.0) + np.where(lo_fin, np.abs(qp.l), 0.0)
     scale_p = 1.0 + max(np.abs(Ax).max(), bnd.max())
     yp, ym = np.maximum(y, 0.0), np.maximum(-y, 0.0)
-    # dual feasibility: positive y only on finite upper bounds, negative only on finite lower
+    # dual feasibility: positive y only on finite upper bounds, negative only on finite lower --
+    # measured against the one-sided rows' own multipliers (a gradient scale set by the equality
+    # rows' multipliers would hide a wrong-signed contact multiplier, qp_exact.solve_exact)
     dual_inf = max(np.where(hi_fin, 0.0, yp).max(), np.where(lo_fin, 0.0, ym).max())
+    one_sided = qp.l != qp.u
+    scale_y = 1.0 + (np.abs(y[one_sided]).max() if one_sided.any() else 0.0)
     gap_hi = np.where(hi_fin, qp.u - Ax, 0.0)
     gap_lo = np.where(lo_fin, Ax - qp.l, 0.0)
     comp = np.maximum(np.abs(yp * gap_hi), np.abs(ym * gap_lo)).max()
     return dict(stationarity=float(np.abs(stat).max() / scale_d),
                 primal=float(viol.max() / scale_p),
-                dual=float(dual_inf / scale_d),
+                dual=float(dual_inf / scale_y),
                 complementarity=float(comp / (scale_d * scale_p)))
 
 
@@ -130,11 +151,14 @@ def _kkt_solve(K, rhs):
     """The working-set KKT system.  When the working set is linearly dependent -- a contact at
     the pyramid apex, where its four pyramid rows and fz >= 0 are all active on three forces --
     K is exactly singular: x is still unique (H > 0), the multipliers are not; least squares
-    returns x and the minimum-norm multipliers."""
+    returns x and the minimum-norm multipliers.  (A nearly singular K can come back from the LU
+    solve finite but wrong: its residual decides.)"""
     try:
         sol = np.linalg.solve(K, rhs)
         if np.all(np.isfinite(sol)):
-            return sol
+            res = np.abs(K @ sol - rhs).max()
+            if res <= 1e-9 * (np.abs(rhs).max() + np.abs(K).max() * np.abs(sol).max()):
+                return sol
     except np.linalg.LinAlgError:
         pass
     return np.linalg.lstsq(K, rhs, rcond=None)[0]
@@ -150,13 +174,15 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
     for (i, sg, bd) in ineq:
         assert sg * (A[i] @ x) < bd, "start point not strictly feasible"
     W: list[int] = []                     # indices into ineq
-    Aeq = A[eq]
+    Aeq, beq = A[eq], qp.u[eq]
+    neq = Aeq.shape[0]
+    degenerate = False
     it = 0
     for it in range(1, max_iter + 1):
         # Solve the equality-constrained QP on the working set directly for its minimiser x_W
         # (more accurate than solving for the step when K is ill-conditioned).
         rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
-        rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
+        rhs_b = np.concatenate([beq] + [[ineq[w][2]] for w in W]) if W else beq
         k = rows.shape[0]
         K = np.zeros((n + k, n + k))
         K[:n, :n] = qp.H
@@ -166,10 +192,22 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
         p, lam = sol[:n] - x, sol[n:]
         if np.abs(p).max() <= 1e-9 * (1.0 + np.abs(x).max()):
             x = sol[:n]
-            lam_in = lam[len(eq):]
-            if len(W) == 0 or lam_in.min() >= -1e-10 * (1.0 + np.abs(lam).max()):
+            lam_in = lam[neq:]
+            # the sign test is relative to the one-sided rows' own multipliers: the equality
+            # multipliers (dynamics, and the wheel rows' ~1e6 when those rows fix dv) would hide
+            # a wrong-signed contact multiplier of the W-scale (1e-4) under a tolerance of 1e-10
+            if len(W) == 0:
                 break
-            W.pop(int(np.argmin(lam_in)))
+            tol_in = 1e-10 * (1.0 + np.abs(lam_in).max())
+            if lam_in.min() >= -tol_in:
+                break
+            # Bland's rule after a degenerate step (alpha = 0: a dependent working set, where the
+            # multipliers are not unique and the most negative one can cycle): the wrong-signed
+            # row of lowest index leaves
+            if degenerate:
+                W.pop(min((j for j in range(len(W)) if lam_in[j] < -tol_in), key=lambda j: W[j]))
+            else:
+                W.pop(int(np.argmin(lam_in)))
             continue
         alpha, block = 1.0, None
         for j, (i, sg, bd) in enumerate(ineq):
@@ -178,8 +216,9 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
             ap = sg * (A[i] @ p)
             if ap > 1e-9 * np.abs(p).max():
                 a = (bd - sg * (A[i] @ x)) / ap
-                if a < alpha:
+                if a < alpha:   # (ties: the lowest index, j ascending -- Bland)
                     alpha, block = max(a, 0.0), j
+        degenerate = block is not None and alpha <= 1e-14
         x = x + alpha * p
         if block is not None:
             W.append(block)
@@ -188,7 +227,7 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
 
     # Final exact KKT solve on the identified active set (removes accumulated step rounding).
     rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
-    rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
+    rhs_b = np.concatenate([beq] + [[ineq[w][2]] for w in W]) if W else beq
     k = rows.shape[0]
     K = np.zeros((n + k, n + k))
     K[:n, :n] = qp.H
@@ -207,14 +246,18 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
         soll = soll + _kkt_solve(K, r.astype(np.float64)).astype(np.longdouble)
     sol = soll.astype(np.float64)
     x, lam = sol[:n], sol[n:]
+    # a degenerate working set whose KKT system came back inconsistent (the active-set method does
+    # not resolve every such case): refuse rather than return a point off the equality rows
+    eq_res = np.abs(A[eq] @ x - qp.u[eq]).max() if eq else 0.0
+    if not eq_res <= 1e-8 * (1.0 + np.abs(qp.u[eq]).max() if eq else 1.0):
+        raise RuntimeError(f"active set ended off the equality rows ({eq_res:.1e})")
     y = np.zeros(A.shape[0])
-    for j, i in enumerate(eq):
-        y[i] += lam[j]
+    y[eq] += lam[:neq]
     active = np.zeros(A.shape[0], bool)
     active[eq] = True
     for j, w in enumerate(W):
         i, sg, _ = ineq[w]
-        y[i] += sg * lam[len(eq) + j]
+        y[i] += sg * lam[neq + j]
         active[i] = True
     cert = kkt_certificate(qp, x, y)
     return ExactSolution(x=x, y=y, active=active, iterations=it, cert=cert)

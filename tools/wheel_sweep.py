@@ -1,8 +1,8 @@
-"""Study of the wheel no-slip rows' interior-point settings (GPU): for each (penalty, row
-tolerance, eps_mu) the convergence status counts, iterations and torque error against the exact
-oracle on a sample of envs.
+"""Study of the wheel no-slip rows' interior-point settings (GPU): for each (row tolerance,
+eps_mu) the convergence status counts, iterations and torque error against the exact oracle on a
+sample of envs.
 
-    python tools/wheel_sweep.py [nenv] [noracle]
+    python tools/wheel_sweep.py [nenv] [noracle] [seed]
 """
 import json
 import os
@@ -27,9 +27,10 @@ nor = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 model = load_model("walter_sr_wheels")
 wheel = WheelRows(dof=np.array(WALTER_WHEEL_DOFS), radius=np.full(8, WHEEL_RADIUS))
 cases = []
+SEED = int(sys.argv[3]) if len(sys.argv) > 3 else 91
 for scen, mm in (("tumbling", "bernoulli"), ("standing", "ones")):
-    d = generate("walter_sr_wheels", nenv, SEED_BASE + 91, scen, mm)
-    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + 92)
+    d = generate("walter_sr_wheels", nenv, SEED_BASE + SEED, scen, mm)
+    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + SEED + 1)
     ref = []
     for e in range(nor):
         args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
@@ -37,10 +38,15 @@ for scen, mm in (("tumbling", "bernoulli"), ("standing", "ones")):
     cases.append((scen, d, wd, np.array(ref)))
 
 from osc_amd.solver import OSCBatchSolver  # noqa: E402
-settings = [(p, t, e) for p in ("1e2", "1e3", "1e4") for t in ("1e-8", "1e-6") for e in ("1e-12", "1e-9")]
-for pen, tol, eps in settings:
-    os.environ["OSC_WHEEL_PENALTY"], os.environ["OSC_WHEEL_TOL"] = pen, tol
-    s = OSCBatchSolver("walter_sr_wheels", YAML, eps_mu=float(eps))
+settings = [(None, None)] + [("1e-6", e) for e in
+                             os.environ.get("SWEEP_EPS", "1e-12,1e-10").split(",")]
+for tol, eps in settings:
+    if tol is None:
+        os.environ.pop("OSC_WHEEL_TOL", None)
+    else:
+        os.environ["OSC_WHEEL_TOL"] = tol
+    s = (OSCBatchSolver("walter_sr_wheels", YAML) if eps is None else
+         OSCBatchSolver("walter_sr_wheels", YAML, eps_mu=float(eps)))
     for scen, d, wd, ref in cases:
         res = s.solve(**d, wheel_dir=wd)
         torch.cuda.synchronize()
@@ -48,8 +54,9 @@ for pen, tol, eps in settings:
         it = res.iters.cpu().numpy()
         tau = res.tau.cpu().numpy()[:nor]
         err = (np.abs(tau - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1.0))
-        print(json.dumps({"penalty": pen, "tol": tol, "eps_mu": eps, "scenario": scen,
+        print(json.dumps({"tol": tol, "eps_mu": eps, "scenario": scen,
                           "status": np.bincount(st, minlength=4).tolist(),
                           "iters_mean": float(it.mean()), "iters_max": int(it.max()),
-                          "err_max": float(err.max()), "err_med": float(np.median(err))}), flush=True)
+                          "err_max": float(err.max()), "err_med": float(np.median(err)),
+                          "not_ok": np.nonzero(st != 0)[0][:20].tolist()}), flush=True)
     s.close()
