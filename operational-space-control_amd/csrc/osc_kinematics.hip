@@ -14,10 +14,12 @@
 //   a_b = (al, a_O)     spatial bias acceleration at zero joint acceleration
 //   I_b = (m, h = m c, I_O)   spatial inertia about the origin; I (w, v) = (I_O w + h x v,
 //                             m v - h x w)
-// A hinge dof has S = (a, p x a) (axis a through anchor p); a free joint's translational dofs
+// A hinge dof has S = (a, p x a) (axis a through anchor p), a slide S = (0, a), a ball's three
+// dofs (R e_k, p x R e_k) (body axes through its anchor); a free joint's translational dofs
 // are (0, e_k) (world axes) and its rotational dofs (R e_k, x x R e_k) (body axes through the
-// body origin: MuJoCo's body-frame angular qvel).  Since S of a hinge is fixed in its parent,
-// dS/dt = v_parent x S, so a_b = a_p + v_p x (S qd); the free root has a = (0, v x w).
+// body origin: MuJoCo's body-frame angular qvel).  Since S of a hinge / slide is fixed in its
+// parent (a ball's in its body, and v_b x S qd = v_p x S qd), a_b = a_p + v_p x (S qd); the free
+// root has a = (0, v x w).
 //   qfrc_bias: f_b = I_b (a_b - (0, g)) + v_b x* I_b v_b, summed over subtrees, C_d = S_d . f.
 //   mj_fullM:  M_ij = S_i . (Ic_{body(j)} S_j) for body(i) an ancestor of body(j) (Ic =
 //              subtree composite inertia), + armature on the diagonal.
@@ -186,30 +188,49 @@ __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
         Rb[3 * i + j] = pR[3 * i] * rq[j] + pR[3 * i + 1] * rq[3 + j] + pR[3 * i + 2] * rq[6 + j];
       x[i] = px[i] + pR[3 * i] * bp[0] + pR[3 * i + 1] * bp[1] + pR[3 * i + 2] * bp[2];
     }
-    if (jt == OSC_KIN_JOINT_HINGE) {
-      const double* u = K->axis[b];
+    if (jt == OSC_KIN_JOINT_HINGE || jt == OSC_KIN_JOINT_BALL) {
+      // rotation about the anchor: R = Rb Ra, the anchor stays put
       const double* jp = K->jpos[b];
-      double anc[3], a[3];
-      for (int i = 0; i < 3; ++i) {
+      double anc[3], Ra[9];
+      for (int i = 0; i < 3; ++i)
         anc[i] = x[i] + Rb[3 * i] * jp[0] + Rb[3 * i + 1] * jp[1] + Rb[3 * i + 2] * jp[2];
-        a[i] = Rb[3 * i] * u[0] + Rb[3 * i + 1] * u[1] + Rb[3 * i + 2] * u[2];
+      if (jt == OSC_KIN_JOINT_HINGE) {
+        // Rodrigues in the body frame: Raa = c I + s [u]x + (1 - c) u u'
+        const double* u = K->axis[b];
+        const double t = 1.0 - c;
+        Ra[0] = c + t * u[0] * u[0]; Ra[1] = t * u[0] * u[1] - s * u[2]; Ra[2] = t * u[0] * u[2] + s * u[1];
+        Ra[3] = t * u[0] * u[1] + s * u[2]; Ra[4] = c + t * u[1] * u[1]; Ra[5] = t * u[1] * u[2] - s * u[0];
+        Ra[6] = t * u[0] * u[2] - s * u[1]; Ra[7] = t * u[1] * u[2] + s * u[0]; Ra[8] = c + t * u[2] * u[2];
+      } else {   // ball: qpos = unit quaternion of the body relative to its parent frame
+        const int qa = K->qadr[b];
+        double qw = q[qa], qx = q[qa + 1], qy = q[qa + 2], qz = q[qa + 3];
+        const double inv = 1.0 / sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+        qw *= inv; qx *= inv; qy *= inv; qz *= inv;
+        Ra[0] = 1 - 2 * (qy * qy + qz * qz); Ra[1] = 2 * (qx * qy - qw * qz); Ra[2] = 2 * (qx * qz + qw * qy);
+        Ra[3] = 2 * (qx * qy + qw * qz); Ra[4] = 1 - 2 * (qx * qx + qz * qz); Ra[5] = 2 * (qy * qz - qw * qx);
+        Ra[6] = 2 * (qx * qz - qw * qy); Ra[7] = 2 * (qy * qz + qw * qx); Ra[8] = 1 - 2 * (qx * qx + qy * qy);
       }
-      // Rodrigues in the body frame: Raa = c I + s [u]x + (1 - c) u u'
-      const double t = 1.0 - c;
-      const double Ra[9] = {c + t * u[0] * u[0], t * u[0] * u[1] - s * u[2], t * u[0] * u[2] + s * u[1],
-                            t * u[0] * u[1] + s * u[2], c + t * u[1] * u[1], t * u[1] * u[2] - s * u[0],
-                            t * u[0] * u[2] - s * u[1], t * u[1] * u[2] + s * u[0], c + t * u[2] * u[2]};
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
           R[3 * i + j] = Rb[3 * i] * Ra[j] + Rb[3 * i + 1] * Ra[3 + j] + Rb[3 * i + 2] * Ra[6 + j];
       for (int i = 0; i < 3; ++i)
         x[i] = anc[i] - (R[3 * i] * jp[0] + R[3 * i + 1] * jp[1] + R[3 * i + 2] * jp[2]);
-      const double qv = qd[K->dadr[b]];
-      double pa[3], wj[3], vj[3];
-      cross(anc, a, pa);
+      // joint motion (wj, vj) = S qd: hinge S = (a, anc x a) with a = Rb u (fixed in the parent);
+      // ball S = (R e_k, anc x R e_k), qd = body-frame angular velocity.  Either S is fixed in the
+      // body, so dS/dt qd = v_b x (S qd) = v_p x (S qd): the same bias terms as the hinge.
+      double wj[3], vj[3];
+      if (jt == OSC_KIN_JOINT_HINGE) {
+        const double* u = K->axis[b];
+        const double qv = qd[K->dadr[b]];
+        for (int i = 0; i < 3; ++i)
+          wj[i] = (Rb[3 * i] * u[0] + Rb[3 * i + 1] * u[1] + Rb[3 * i + 2] * u[2]) * qv;
+      } else {
+        const int da = K->dadr[b];
+        const double wl[3] = {qd[da], qd[da + 1], qd[da + 2]};
+        for (int i = 0; i < 3; ++i) wj[i] = R[3 * i] * wl[0] + R[3 * i + 1] * wl[1] + R[3 * i + 2] * wl[2];
+      }
+      cross(anc, wj, vj);
       for (int i = 0; i < 3; ++i) {
-        wj[i] = a[i] * qv;
-        vj[i] = pa[i] * qv;
         w[i] = pw[i] + wj[i];
         vo[i] = pvo[i] + vj[i];
       }
@@ -220,6 +241,21 @@ __device__ void body_forward(const KinDev* K, double* E, const EnvLayout& lay,
       for (int i = 0; i < 3; ++i) {
         al[i] = pal[i] + c1[i];
         ao[i] = pao[i] + c2[i] + c3[i];
+      }
+    } else if (jt == OSC_KIN_JOINT_SLIDE) {
+      // translation along a = Rb u (fixed in the parent): S = (0, a), bias v_p x (0, a qd)
+      const double* u = K->axis[b];
+      const double qv = q[K->qadr[b]], qdv = qd[K->dadr[b]];
+      double vj[3], c2[3];
+      for (int i = 0; i < 3; ++i) {
+        const double a = Rb[3 * i] * u[0] + Rb[3 * i + 1] * u[1] + Rb[3 * i + 2] * u[2];
+        x[i] += a * qv;
+        vj[i] = a * qdv;
+      }
+      for (int i = 0; i < 9; ++i) R[i] = Rb[i];
+      cross(pw, vj, c2);
+      for (int i = 0; i < 3; ++i) {
+        w[i] = pw[i]; vo[i] = pvo[i] + vj[i]; al[i] = pal[i]; ao[i] = pao[i] + c2[i];
       }
     } else {   // welded to the parent
       for (int i = 0; i < 9; ++i) R[i] = Rb[i];
@@ -370,12 +406,19 @@ __global__ __launch_bounds__(kWave) void osc_kinematics_kernel(
         S[0] = a[0]; S[1] = a[1]; S[2] = a[2];
         cross(xo, a, S + 3);
       }
-    } else {   // hinge: the axis is invariant under its own rotation, so a = R u
+    } else if (K->jtype[bb] == OSC_KIN_JOINT_SLIDE) {   // (0, a), a = R u
+      const double* u = K->axis[bb];
+      S[0] = S[1] = S[2] = 0.0;
+      for (int i = 0; i < 3; ++i)
+        S[3 + i] = B[B_R + 3 * i] * u[0] + B[B_R + 3 * i + 1] * u[1] + B[B_R + 3 * i + 2] * u[2];
+    } else {   // hinge (a = R u: the axis is invariant under its own rotation) or ball (a = R e_k)
       const double* u = K->axis[bb];
       const double* jp = K->jpos[bb];
+      const bool ball = K->jtype[bb] == OSC_KIN_JOINT_BALL;
       double a[3], pa[3];
       for (int i = 0; i < 3; ++i) {
-        a[i] = B[B_R + 3 * i] * u[0] + B[B_R + 3 * i + 1] * u[1] + B[B_R + 3 * i + 2] * u[2];
+        a[i] = ball ? B[B_R + 3 * i + k]
+                    : B[B_R + 3 * i] * u[0] + B[B_R + 3 * i + 1] * u[1] + B[B_R + 3 * i + 2] * u[2];
         pa[i] = B[B_X + i] + B[B_R + 3 * i] * jp[0] + B[B_R + 3 * i + 1] * jp[1] +
                 B[B_R + 3 * i + 2] * jp[2];
       }
@@ -550,7 +593,8 @@ int build_tables(const osc_kin_desc& d, KinDev* k) {
     const int p = d.parent[b];
     if (p < -1 || p >= b) return OSC_ERR_INVALID_ARGUMENT;   // parents first (MuJoCo order)
     const int jt = d.jnt_type[b];
-    if (jt != OSC_KIN_JOINT_NONE && jt != OSC_KIN_JOINT_FREE && jt != OSC_KIN_JOINT_HINGE)
+    if (jt != OSC_KIN_JOINT_NONE && jt != OSC_KIN_JOINT_FREE && jt != OSC_KIN_JOINT_BALL &&
+        jt != OSC_KIN_JOINT_SLIDE && jt != OSC_KIN_JOINT_HINGE)
       return OSC_ERR_INVALID_ARGUMENT;
     if (jt == OSC_KIN_JOINT_FREE && p != -1) return OSC_ERR_INVALID_ARGUMENT;
     if (!(d.mass[b] >= 0.0) || !(d.armature[b] >= 0.0)) return OSC_ERR_INVALID_ARGUMENT;
@@ -574,7 +618,10 @@ int build_tables(const osc_kin_desc& d, KinDev* k) {
     if (jt == OSC_KIN_JOINT_FREE) {
       nq += 7;
       ndof = 6;
-    } else if (jt == OSC_KIN_JOINT_HINGE) {
+    } else if (jt == OSC_KIN_JOINT_BALL) {
+      nq += 4;
+      ndof = 3;
+    } else if (jt == OSC_KIN_JOINT_HINGE || jt == OSC_KIN_JOINT_SLIDE) {
       nq += 1;
       ndof = 1;
       const double an = std::sqrt(d.axis[b][0] * d.axis[b][0] + d.axis[b][1] * d.axis[b][1] +
@@ -805,6 +852,8 @@ extern "C" int osc_kin_desc_from_json(const char* robot, const char* json_path,
     desc->parent[b] = static_cast<int32_t>(parent);
     if (jt->str == "free") desc->jnt_type[b] = OSC_KIN_JOINT_FREE;
     else if (jt->str == "hinge") desc->jnt_type[b] = OSC_KIN_JOINT_HINGE;
+    else if (jt->str == "slide") desc->jnt_type[b] = OSC_KIN_JOINT_SLIDE;
+    else if (jt->str == "ball") desc->jnt_type[b] = OSC_KIN_JOINT_BALL;
     else if (jt->str == "none") desc->jnt_type[b] = OSC_KIN_JOINT_NONE;
     else return OSC_ERR_IO;
     if (B.get("axis") && !jnums(B.get("axis"), desc->axis[b], 3)) return OSC_ERR_IO;

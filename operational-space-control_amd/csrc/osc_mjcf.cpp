@@ -158,6 +158,65 @@ class XmlParser {
   size_t p_ = 0;
 };
 
+// <include file="..."/>: the included file's <mujoco> children replace the element, wherever it
+// sits (MuJoCo's xml_util include expansion); file names are relative to the main model file's
+// directory.  Nested includes are expanded too (depth-limited, so a cycle is an error).
+bool read_text(const std::string& path, std::string* out) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return false;
+  std::stringstream ss;
+  ss << in.rdbuf();
+  *out = ss.str();
+  return true;
+}
+
+bool expand_includes(XNode* node, const std::string& dir, int depth, std::string* err) {
+  std::vector<std::unique_ptr<XNode>> kids;
+  for (auto& kp : node->kids) {
+    if (kp->tag != "include") {
+      if (!expand_includes(kp.get(), dir, depth, err)) return false;
+      kids.push_back(std::move(kp));
+      continue;
+    }
+    const std::string* f = kp->get("file");
+    if (!f || f->empty()) {
+      *err = "<include> without file";
+      return false;
+    }
+    if (depth >= 16) {
+      *err = "<include> nesting too deep (cycle?) at " + *f;
+      return false;
+    }
+    const std::string path = (!f->empty() && (*f)[0] == '/') ? *f : dir + "/" + *f;
+    std::string text;
+    if (!read_text(path, &text)) {
+      *err = "cannot open included file " + path;
+      return false;
+    }
+    std::string perr;
+    XmlParser parser(text);
+    std::unique_ptr<XNode> root = parser.parse(&perr);
+    if (!root) {
+      *err = path + ": " + perr;
+      return false;
+    }
+    XNode* mj = nullptr;
+    for (auto& k : root->kids)
+      if (k->tag == "mujoco") mj = k.get();
+    if (!mj) {
+      *err = path + ": included file has no <mujoco> element";
+      return false;
+    }
+    if (!expand_includes(mj, dir, depth + 1, err)) return false;
+    for (auto& k : mj->kids) {
+      k->parent = node;
+      kids.push_back(std::move(k));
+    }
+  }
+  node->kids.swap(kids);
+  return true;
+}
+
 // ------------------------------------------------------------------ small math
 struct Quat {
   double w = 1, x = 0, y = 0, z = 0;
@@ -246,6 +305,8 @@ bool nums(const std::string* s, double* out, int n) {
 struct Compiler {
   bool degree = true;            // MuJoCo's default angle unit
   std::string eulerseq = "xyz";
+  int inertiafromgeom = 2;       // 0 false, 1 true, 2 auto (MuJoCo's default)
+  int group_lo = 0, group_hi = 5;   // inertiagrouprange
 };
 
 struct DefaultClass {
@@ -281,6 +342,39 @@ void quat2mat(const double* q, double* R) {
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
   R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
   R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+// one <joint> / <freejoint> as written (its class defaults resolved)
+struct JointSpec {
+  int type = OSC_KIN_JOINT_HINGE;
+  double axis[3] = {0.0, 0.0, 1.0};
+  double pos[3] = {0.0, 0.0, 0.0};
+  double armature = 0.0;
+};
+
+// mass, COM and inertia about the COM (body frame) of one geom or a sum of them
+struct MassProps {
+  double m = 0.0, c[3] = {0.0, 0.0, 0.0}, I[9] = {0.0};
+};
+
+// a += b: combined mass, COM and inertia about the combined COM (parallel-axis theorem)
+void mass_add(MassProps* a, const MassProps& b) {
+  const double m = a->m + b.m;
+  if (!(m > 0.0)) return;
+  double c[3];
+  for (int i = 0; i < 3; ++i) c[i] = (a->m * a->c[i] + b.m * b.c[i]) / m;
+  double I[9];
+  for (int k = 0; k < 9; ++k) I[k] = a->I[k] + b.I[k];
+  const MassProps* parts[2] = {a, &b};
+  for (const MassProps* q : parts) {
+    const double dv[3] = {q->c[0] - c[0], q->c[1] - c[1], q->c[2] - c[2]};
+    const double dd = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) I[3 * i + j] += q->m * ((i == j ? dd : 0.0) - dv[i] * dv[j]);
+  }
+  a->m = m;
+  for (int i = 0; i < 3; ++i) a->c[i] = c[i];
+  for (int k = 0; k < 9; ++k) a->I[k] = I[k];
 }
 
 struct Loader {
@@ -404,28 +498,221 @@ struct Loader {
     return true;
   }
 
-  bool body(const XNode& n, int parent, const DefaultClass* active) {
+  int new_body(int parent, const std::string& name) {
     const int b = d->nbody;
-    if (b >= kMaxRaw) return fail("too many bodies");
+    if (b >= kMaxRaw) {
+      fail("too many bodies");
+      return -1;
+    }
     ++d->nbody;
-    const std::string* nm = n.get("name");
-    body_name.push_back(nm ? *nm : "");
+    body_name.push_back(name);
     d->parent[b] = parent;
     d->jnt_type[b] = OSC_KIN_JOINT_NONE;
     d->quat[b][0] = 1.0;
     d->iquat[b][0] = 1.0;
     d->axis[b][2] = 1.0;
+    return b;
+  }
+
+  bool joint(const XNode& k, const DefaultClass* active, JointSpec* j) {
+    const DefaultClass* c = cls_of(k, active);
+    if (!err.empty()) return false;
+    std::string type = k.tag == "freejoint" ? "free" : "hinge";
+    if (k.tag == "joint")
+      if (const std::string* t = attr(k, c, "type")) type = *t;
+    if (type == "free") j->type = OSC_KIN_JOINT_FREE;
+    else if (type == "ball") j->type = OSC_KIN_JOINT_BALL;
+    else if (type == "slide") j->type = OSC_KIN_JOINT_SLIDE;
+    else if (type == "hinge") j->type = OSC_KIN_JOINT_HINGE;
+    else return fail("unsupported joint type " + type);
+    if (j->type == OSC_KIN_JOINT_HINGE || j->type == OSC_KIN_JOINT_SLIDE)
+      if (const std::string* a = attr(k, c, "axis"))
+        if (!nums(a, j->axis, 3)) return fail("bad joint axis");
+    if (j->type != OSC_KIN_JOINT_FREE)
+      if (const std::string* p = attr(k, c, "pos"))
+        if (!nums(p, j->pos, 3)) return fail("bad joint pos");
+    if (const std::string* a = attr(k, c, "armature"))
+      if (!nums(a, &j->armature, 1)) return fail("bad armature");
+    // ref shifts qpos0 (the pose is computed at q - ref): not modelled, so refused
+    if (const std::string* r = attr(k, c, "ref")) {
+      double v = 0.0;
+      if (!nums(r, &v, 1)) return fail("bad joint ref");
+      if (v != 0.0) return fail("joint ref != 0 unsupported (qpos0 offset)");
+    }
+    return true;
+  }
+
+  // MuJoCo's geom mass properties (mjCGeom: density 1000 unless mass is given, principal
+  // inertia of the primitive about its centre, placed by pos / orientation | fromto).
+  // `used` = false for geoms outside inertiagrouprange (ignored, as MuJoCo does).
+  bool geom_mass(const XNode& g, const DefaultClass* active, MassProps* out, bool* used) {
+    const DefaultClass* c = cls_of(g, active);
+    if (!err.empty()) return false;
+    *used = false;
+    double grp = 0.0;
+    if (const std::string* s = attr(g, c, "group"))
+      if (!nums(s, &grp, 1)) return fail("bad geom group");
+    if (grp < comp.group_lo || grp > comp.group_hi) return true;
+    *used = true;
+    std::string type = "sphere";
+    if (const std::string* t = attr(g, c, "type")) type = *t;
+    if (type == "mesh" || type == "sdf" || type == "hfield")
+      return fail("inertia from " + type + " geoms unsupported (give the body an <inertial>)");
+    if (type == "plane") return fail("plane geom in a moving body");
+    double size[3] = {0.0, 0.0, 0.0};
+    if (const std::string* sz = attr(g, c, "size")) {
+      std::istringstream in(*sz);
+      int n = 0;
+      while (n < 3 && (in >> size[n])) ++n;
+    }
+    double pos[3] = {0.0, 0.0, 0.0};
+    Quat q;
+    if (const std::string* ft = attr(g, c, "fromto")) {
+      if (type != "capsule" && type != "cylinder" && type != "box" && type != "ellipsoid")
+        return fail("fromto on a " + type + " geom");
+      double v[6];
+      if (!nums(ft, v, 6)) return fail("bad geom fromto");
+      const double dz[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+      const double len = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
+      if (!(len > 0.0)) return fail("degenerate geom fromto");
+      for (int i = 0; i < 3; ++i) pos[i] = 0.5 * (v[i] + v[3 + i]);
+      // half-length along the geom's z: size[1] (capsule, cylinder) or size[2] (box, ellipsoid)
+      size[(type == "capsule" || type == "cylinder") ? 1 : 2] = 0.5 * len;
+      const double z[3] = {dz[0] / len, dz[1] / len, dz[2] / len};
+      const double ax[3] = {-z[1], z[0], 0.0};
+      const double s2 = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1]);
+      q = s2 < 1e-14 ? (z[2] > 0 ? Quat{} : Quat{0, 1, 0, 0}) : axis_angle(ax, std::atan2(s2, z[2]));
+    } else {
+      if (const std::string* p = attr(g, c, "pos"))
+        if (!nums(p, pos, 3)) return fail("bad geom pos");
+      if (!orientation(g, c, &q)) return false;
+    }
+    double vol = 0.0, Id[3] = {0.0, 0.0, 0.0};   // volume; principal inertia per unit mass
+    const double r = size[0];
+    if (type == "sphere") {
+      vol = 4.0 / 3.0 * M_PI * r * r * r;
+      Id[0] = Id[1] = Id[2] = 0.4 * r * r;
+    } else if (type == "capsule" || type == "cylinder") {
+      const double h = size[1], H = 2.0 * h;
+      const double vc = M_PI * r * r * H;
+      if (type == "cylinder") {
+        vol = vc;
+        Id[0] = Id[1] = (3.0 * r * r + H * H) / 12.0;
+        Id[2] = 0.5 * r * r;
+      } else {   // cylinder + two hemispheres (each's COM 3r/8 off its flat face)
+        const double vs = 4.0 / 3.0 * M_PI * r * r * r;
+        vol = vc + vs;
+        const double Ixc = vc * (3.0 * r * r + H * H) / 12.0;
+        const double Ixs = vs * (0.4 * r * r + h * h + 0.75 * h * r);
+        Id[0] = Id[1] = (Ixc + Ixs) / vol;
+        Id[2] = (vc * 0.5 * r * r + vs * 0.4 * r * r) / vol;
+      }
+    } else if (type == "box") {
+      vol = 8.0 * size[0] * size[1] * size[2];
+      Id[0] = (size[1] * size[1] + size[2] * size[2]) / 3.0;
+      Id[1] = (size[0] * size[0] + size[2] * size[2]) / 3.0;
+      Id[2] = (size[0] * size[0] + size[1] * size[1]) / 3.0;
+    } else if (type == "ellipsoid") {
+      vol = 4.0 / 3.0 * M_PI * size[0] * size[1] * size[2];
+      Id[0] = (size[1] * size[1] + size[2] * size[2]) / 5.0;
+      Id[1] = (size[0] * size[0] + size[2] * size[2]) / 5.0;
+      Id[2] = (size[0] * size[0] + size[1] * size[1]) / 5.0;
+    } else {
+      return fail("unsupported geom type " + type);
+    }
+    double mass = 0.0;
+    if (const std::string* ms = attr(g, c, "mass")) {
+      if (!nums(ms, &mass, 1) || mass < 0.0) return fail("bad geom mass");
+    } else {
+      double rho = 1000.0;
+      if (const std::string* dn = attr(g, c, "density"))
+        if (!nums(dn, &rho, 1) || rho < 0.0) return fail("bad geom density");
+      mass = rho * vol;
+    }
+    if (mass > 0.0 && !(vol > 0.0)) return fail("geom with mass but no volume");
+    if (const std::string* sh = attr(g, c, "shellinertia"))
+      if (*sh == "true") return fail("shellinertia unsupported");
+    double R[9];
+    const double qa[4] = {q.w, q.x, q.y, q.z};
+    quat2mat(qa, R);
+    out->m = mass;
+    for (int i = 0; i < 3; ++i) out->c[i] = pos[i];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double t = 0.0;
+        for (int k = 0; k < 3; ++k) t += R[3 * i + k] * Id[k] * R[3 * j + k];
+        out->I[3 * i + j] = mass * t;
+      }
+    return true;
+  }
+
+  // principal frame of a body-frame inertia tensor -> ipos / iquat / inertia of body b
+  void set_inertia(int b, const MassProps& mp) {
+    double lam[3], V[9];
+    eig3(mp.I, lam, V);
+    const double det = V[0] * (V[4] * V[8] - V[5] * V[7]) - V[1] * (V[3] * V[8] - V[5] * V[6]) +
+                       V[2] * (V[3] * V[7] - V[4] * V[6]);
+    if (det < 0)
+      for (int i = 0; i < 3; ++i) V[3 * i + 2] = -V[3 * i + 2];
+    const Quat iq = mat2quat(V);
+    d->mass[b] = mp.m;
+    for (int i = 0; i < 3; ++i) {
+      d->ipos[b][i] = mp.c[i];
+      d->inertia[b][i] = lam[i] < 0.0 ? 0.0 : lam[i];
+    }
+    d->iquat[b][0] = iq.w; d->iquat[b][1] = iq.x; d->iquat[b][2] = iq.y; d->iquat[b][3] = iq.z;
+  }
+
+  // A body with k > 1 joints becomes a chain of k bodies, one joint each, exactly as
+  // mj_kinematics composes a body's joints in order: the first carries the body's frame
+  // (pos, orientation), the others sit at zero offset in the frame the previous joint left,
+  // and the last (the body proper: its name, inertia, sites, children) gets everything else.
+  // The leading chain bodies are massless.
+  bool body(const XNode& n, int parent, const DefaultClass* active) {
+    const std::string* nm = n.get("name");
+    const std::string name = nm ? *nm : "";
     if (const std::string* cc = n.get("childclass")) {
       auto it = classes.find(*cc);
       if (it == classes.end()) return fail("unknown childclass " + *cc);
       active = it->second.get();
     }
+    std::vector<JointSpec> js;
+    for (const auto& kp : n.kids)
+      if (kp->tag == "joint" || kp->tag == "freejoint") {
+        js.emplace_back();
+        if (!joint(*kp, active, &js.back())) return false;
+      }
+    for (size_t i = 0; i < js.size(); ++i) {
+      if (js[i].type == OSC_KIN_JOINT_FREE && (js.size() > 1 || parent >= 0))
+        return fail("free joint must be the only joint of a top-level body (" + name + ")");
+      // MuJoCo's ball dofs turn about the body's FINAL axes (mj_comPos); they are the ball's own
+      // only when no rotating joint follows it on the body
+      if (js[i].type == OSC_KIN_JOINT_BALL)
+        for (size_t k = i + 1; k < js.size(); ++k)
+          if (js[k].type == OSC_KIN_JOINT_BALL || js[k].type == OSC_KIN_JOINT_HINGE)
+            return fail("ball joint followed by a rotating joint on body " + name);
+    }
+    int b = new_body(parent, js.size() > 1 ? "" : name);
+    if (b < 0) return false;
     if (n.get("pos") && !nums(n.get("pos"), d->pos[b], 3)) return fail("bad body pos");
     Quat q;
     if (!orientation(n, nullptr, &q)) return false;
     d->quat[b][0] = q.w; d->quat[b][1] = q.x; d->quat[b][2] = q.y; d->quat[b][3] = q.z;
-    bool inertial = false, geoms = false;
-    int njoint = 0;
+    for (size_t i = 0; i < js.size(); ++i) {
+      if (i > 0) {
+        b = new_body(b, i + 1 == js.size() ? name : "");
+        if (b < 0) return false;
+      }
+      d->jnt_type[b] = js[i].type;
+      for (int t = 0; t < 3; ++t) {
+        d->axis[b][t] = js[i].axis[t];
+        d->jnt_pos[b][t] = js[i].pos[t];
+      }
+      d->armature[b] = js[i].armature;
+    }
+    bool inertial = false;
+    MassProps from_geoms;
+    int ngeom = 0;
     for (const auto& kp : n.kids) {
       const XNode& k = *kp;
       if (k.tag == "inertial") {
@@ -454,39 +741,39 @@ struct Loader {
           return fail("inertial needs diaginertia or fullinertia");
         }
         d->iquat[b][0] = iq.w; d->iquat[b][1] = iq.x; d->iquat[b][2] = iq.y; d->iquat[b][3] = iq.z;
-      } else if (k.tag == "joint" || k.tag == "freejoint") {
-        if (++njoint > 1) return fail("more than one joint on body " + body_name[b]);
-        const DefaultClass* c = cls_of(k, active);
-        if (!err.empty()) return false;
-        std::string type = k.tag == "freejoint" ? "free" : "hinge";
-        if (k.tag == "joint")
-          if (const std::string* t = attr(k, c, "type")) type = *t;
-        if (type == "free") {
-          d->jnt_type[b] = OSC_KIN_JOINT_FREE;
-        } else if (type == "hinge") {
-          d->jnt_type[b] = OSC_KIN_JOINT_HINGE;
-          if (const std::string* a = attr(k, c, "axis"))
-            if (!nums(a, d->axis[b], 3)) return fail("bad joint axis");
-          if (const std::string* p = attr(k, c, "pos"))
-            if (!nums(p, d->jnt_pos[b], 3)) return fail("bad joint pos");
-        } else {
-          return fail("unsupported joint type " + type);
-        }
-        if (const std::string* a = attr(k, c, "armature"))
-          if (!nums(a, &d->armature[b], 1)) return fail("bad armature");
       } else if (k.tag == "site") {
         if (!site(k, b, active)) return false;
       } else if (k.tag == "geom") {
-        geoms = true;
+        // mass properties are needed only under inertiafromgeom true, or auto without <inertial>
+        // (decided below); an unsupported geom is an error only if it would be used
+        if (comp.inertiafromgeom == 0) continue;
+        MassProps g;
+        bool used = false;
+        if (!geom_mass(k, active, &g, &used)) {
+          if (comp.inertiafromgeom == 1 || !has_inertial(n)) return false;
+          err.clear();
+          continue;
+        }
+        if (used) {
+          mass_add(&from_geoms, g);
+          ++ngeom;
+        }
       } else if (k.tag == "frame" || k.tag == "include" || k.tag == "replicate" ||
                  k.tag == "composite" || k.tag == "flexcomp") {
-        return fail("unsupported <" + k.tag + "> in body " + body_name[b]);
+        return fail("unsupported <" + k.tag + "> in body " + name);
       }
     }
-    if (!inertial && geoms) return fail("body " + body_name[b] + " has no <inertial> (inertia from geoms unsupported)");
+    if (ngeom > 0 && (comp.inertiafromgeom == 1 || (comp.inertiafromgeom == 2 && !inertial)))
+      set_inertia(b, from_geoms);
     for (const auto& kp : n.kids)
       if (kp->tag == "body" && !body(*kp, b, active)) return false;
     return true;
+  }
+
+  static bool has_inertial(const XNode& n) {
+    for (const auto& kp : n.kids)
+      if (kp->tag == "inertial") return true;
+    return false;
   }
 
   bool site(const XNode& k, int b, const DefaultClass* active) {
@@ -523,14 +810,29 @@ struct Loader {
           else return fail("bad compiler angle");
         }
         if (const std::string* e = k.get("eulerseq")) comp.eulerseq = *e;
-        if (const std::string* ig = k.get("inertiafromgeom"))
-          if (*ig == "true") return fail("inertiafromgeom=\"true\" unsupported");
+        if (const std::string* ig = k.get("inertiafromgeom")) {
+          if (*ig == "false") comp.inertiafromgeom = 0;
+          else if (*ig == "true") comp.inertiafromgeom = 1;
+          else if (*ig == "auto") comp.inertiafromgeom = 2;
+          else return fail("bad compiler inertiafromgeom");
+        }
+        if (const std::string* gr = k.get("inertiagrouprange")) {
+          double v[2];
+          if (!nums(gr, v, 2)) return fail("bad compiler inertiagrouprange");
+          comp.group_lo = static_cast<int>(v[0]);
+          comp.group_hi = static_cast<int>(v[1]);
+        }
+        // options that rescale or clamp masses are not modelled: refused rather than ignored
+        for (const char* a : {"settotalmass", "boundmass", "boundinertia"})
+          if (const std::string* v = k.get(a)) {
+            double x = 0.0;
+            if (!nums(v, &x, 1) || (std::strcmp(a, "settotalmass") == 0 ? x > 0.0 : x != 0.0))
+              return fail(std::string("compiler ") + a + " unsupported");
+          }
       } else if (k.tag == "option") {
         if (k.get("gravity") && !nums(k.get("gravity"), d->gravity, 3)) return fail("bad gravity");
       } else if (k.tag == "default") {
         if (!read_defaults(k, nullptr)) return false;
-      } else if (k.tag == "include") {
-        return fail("<include> unsupported");
       }
     }
     if (!classes.count("main")) classes["main"] = std::make_unique<DefaultClass>();
@@ -684,17 +986,20 @@ extern "C" int osc_kin_desc_from_mjcf(const char* xml_path, const char* const* b
       (site_order == OSC_MJCF_SITES_BY_NAME && !site_names) ||
       (site_order != OSC_MJCF_SITES_BY_NAME && site_order != OSC_MJCF_SITES_MODEL_ORDER))
     return OSC_ERR_INVALID_ARGUMENT;
-  std::ifstream in(xml_path, std::ios::binary);
-  if (!in) {
+  std::string text;
+  if (!read_text(xml_path, &text)) {
     std::fprintf(stderr, "osc_kin_desc_from_mjcf: cannot open %s\n", xml_path);
     return OSC_ERR_IO;
   }
-  std::stringstream ss;
-  ss << in.rdbuf();
-  const std::string text = ss.str();
   std::string err;
   XmlParser parser(text);
   std::unique_ptr<XNode> root = parser.parse(&err);
+  if (root) {
+    const std::string xp(xml_path);
+    const size_t slash = xp.rfind('/');
+    if (!expand_includes(root.get(), slash == std::string::npos ? "." : xp.substr(0, slash), 0, &err))
+      root.reset();
+  }
   Loader L;
   auto raw = std::make_unique<RawDesc>();
   L.d = raw.get();

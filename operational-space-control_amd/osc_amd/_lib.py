@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
 OSC_KIN_MAX_SITES = 32
-JOINT_NONE, JOINT_FREE, JOINT_HINGE = -1, 0, 3     # MuJoCo's mjtJoint values
+JOINT_NONE, JOINT_FREE, JOINT_BALL, JOINT_SLIDE, JOINT_HINGE = -1, 0, 1, 2, 3   # mjtJoint
 
 
 class OscModelDesc(ctypes.Structure):
@@ -228,7 +228,8 @@ def kin_desc_from_dict(tree: dict) -> OscKinDesc:
     bodies, sites = tree["bodies"], tree["sites"]
     d.nbody, d.nsite = len(bodies), len(sites)
     d.gravity[:] = tree["gravity"]
-    jt = {"free": JOINT_FREE, "hinge": JOINT_HINGE, "none": JOINT_NONE}
+    jt = {"free": JOINT_FREE, "ball": JOINT_BALL, "slide": JOINT_SLIDE, "hinge": JOINT_HINGE,
+          "none": JOINT_NONE}
     for i, b in enumerate(bodies):
         d.parent[i] = b["parent"]
         d.jnt_type[i] = jt[b["joint"]]
@@ -252,7 +253,8 @@ def kin_desc_from_dict(tree: dict) -> OscKinDesc:
 
 def kin_desc_to_dict(d: OscKinDesc, name: str = "") -> dict:
     """The <robot>_kinematics.json schema of a descriptor (inverse of kin_desc_from_dict)."""
-    jt = {JOINT_FREE: "free", JOINT_HINGE: "hinge", JOINT_NONE: "none"}
+    jt = {JOINT_FREE: "free", JOINT_BALL: "ball", JOINT_SLIDE: "slide", JOINT_HINGE: "hinge",
+          JOINT_NONE: "none"}
     bodies = []
     for i in range(d.nbody):
         bodies.append({"parent": d.parent[i], "joint": jt[d.jnt_type[i]], "pos": list(d.pos[i]),

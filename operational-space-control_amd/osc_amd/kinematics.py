@@ -185,25 +185,43 @@ class KinematicsBatch:
             return self.solve_into(solver, out, qpos, qvel, T, mask, ws)
 
 
+def _tree_joints(tree: dict):
+    """(type, body) of every joint in qpos order: a body's "joints" list, else its "joint"."""
+    out = []
+    for i, b in enumerate(tree["bodies"]):
+        if "joints" in b:
+            out += [(j["type"], i) for j in b["joints"]]
+        elif b["joint"] != "none":
+            out.append((b["joint"], i))
+    return out
+
+
 def random_states(tree: dict, nenv: int, seed: int, base_pos_zero: bool = True,
                   joint_range: float = 1.0, vel_scale: float = 1.0):
-    """Seeded synthetic joint states for a tree: unit base quaternion, joint angles uniform in
-    +-joint_range, velocities N(0, vel_scale^2); base position 0 as update_mj_data sets it
-    (osc.h:358-359) unless base_pos_zero is False."""
+    """Seeded synthetic joint states for a tree: unit base / ball quaternions, hinge angles
+    uniform in +-joint_range, slides in +-0.3 joint_range, velocities N(0, vel_scale^2); base
+    position 0 as update_mj_data sets it (osc.h:358-359) unless base_pos_zero is False."""
     rng = np.random.default_rng(seed)
-    nq = sum({"free": 7, "hinge": 1}.get(b["joint"], 0) for b in tree["bodies"])
-    nv = sum({"free": 6, "hinge": 1}.get(b["joint"], 0) for b in tree["bodies"])
+    joints = _tree_joints(tree)
+    nqj = {"free": 7, "ball": 4, "slide": 1, "hinge": 1}
+    nvj = {"free": 6, "ball": 3, "slide": 1, "hinge": 1}
+    nq = sum(nqj[t] for t, _ in joints)
+    nv = sum(nvj[t] for t, _ in joints)
     qpos = np.zeros((nenv, nq))
     qvel = vel_scale * rng.standard_normal((nenv, nv))
     qa = 0
-    for b in tree["bodies"]:
-        if b["joint"] == "free":
+    for t, _ in joints:
+        if t == "free":
             if not base_pos_zero:
                 qpos[:, qa:qa + 3] = 0.3 * rng.standard_normal((nenv, 3))
             q = rng.standard_normal((nenv, 4))
             qpos[:, qa + 3:qa + 7] = q / np.linalg.norm(q, axis=1, keepdims=True)
-            qa += 7
-        elif b["joint"] == "hinge":
+        elif t == "ball":
+            q = rng.standard_normal((nenv, 4))
+            qpos[:, qa:qa + 4] = q / np.linalg.norm(q, axis=1, keepdims=True)
+        elif t == "hinge":
             qpos[:, qa] = rng.uniform(-joint_range, joint_range, size=nenv)
-            qa += 1
+        else:
+            qpos[:, qa] = rng.uniform(-0.3 * joint_range, 0.3 * joint_range, size=nenv)
+        qa += nqj[t]
     return qpos, qvel

@@ -48,15 +48,20 @@ def tree_to_mjcf(tree: dict, body_names=None, site_names=None, extra_bodies=(),
             out.append(f'{sp}<body name="{bn[i]}" pos="{_fmt(b["pos"])}" quat="{_fmt(b["quat"])}">')
             out.append(f'{sp}  <inertial pos="{_fmt(b["ipos"])}" quat="{_fmt(b["iquat"])}" '
                        f'mass="{float(b["mass"])!r}" diaginertia="{_fmt(b["diaginertia"])}"/>')
-            if b["joint"] == "free":
-                arm = b.get("armature", 0.0)
-                out.append(f'{sp}  <freejoint name="{bn[i]}_root"/>' if not arm else
-                           f'{sp}  <joint name="{bn[i]}_root" type="free" armature="{float(arm)!r}"/>')
-            elif b["joint"] == "hinge":
-                out.append(f'{sp}  <joint name="{bn[i]}_joint" type="hinge" '
-                           f'axis="{_fmt(b.get("axis", [0, 0, 1]))}" '
-                           f'pos="{_fmt(b.get("jnt_pos", [0, 0, 0]))}" '
-                           f'armature="{float(b.get("armature", 0.0))!r}"/>')
+            joints = b["joints"] if "joints" in b else (
+                [] if b["joint"] == "none" else
+                [dict(type=b["joint"], axis=b.get("axis", [0, 0, 1]),
+                      pos=b.get("jnt_pos", [0, 0, 0]), armature=b.get("armature", 0.0))])
+            for n, j in enumerate(joints):
+                jn = f"{bn[i]}_joint" if n == 0 else f"{bn[i]}_joint{n}"
+                arm = float(j.get("armature", 0.0))
+                if j["type"] == "free":
+                    out.append(f'{sp}  <freejoint name="{bn[i]}_root"/>' if not arm else
+                               f'{sp}  <joint name="{bn[i]}_root" type="free" armature="{arm!r}"/>')
+                    continue
+                ax = f' axis="{_fmt(j.get("axis", [0, 0, 1]))}"' if j["type"] != "ball" else ""
+                out.append(f'{sp}  <joint name="{jn}" type="{j["type"]}"{ax} '
+                           f'pos="{_fmt(j.get("pos", [0, 0, 0]))}" armature="{arm!r}"/>')
         for k in sites_of.get(i, []):
             out.append(f'{sp}  <site name="{sn[k]}" pos="{_fmt(tree["sites"][k]["pos"])}"/>')
         for c in children[i]:

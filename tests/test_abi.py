@@ -164,7 +164,9 @@ def test_kin_desc_errors():
     bad = [lambda d: setattr(d, "nbody", 17),
            lambda d: d.parent.__setitem__(3, 5),            # parent after child
            lambda d: d.jnt_type.__setitem__(2, 0),          # free joint below the root
-           lambda d: d.jnt_type.__setitem__(2, 2),          # slide: not supported
+           lambda d: d.jnt_type.__setitem__(2, 5),          # not an mjtJoint value
+           lambda d: [d.jnt_type.__setitem__(1, 2)] +       # slide without an axis
+                     [d.axis[1].__setitem__(i, 0.0) for i in range(3)],
            lambda d: d.site_body.__setitem__(0, 40),
            lambda d: [d.axis[1].__setitem__(i, 0.0) for i in range(3)]]
     for mutate in bad:

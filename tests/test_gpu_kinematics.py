@@ -12,7 +12,8 @@ import pytest
 torch = pytest.importorskip("torch")
 
 import kinematics as kin
-from kin_trees import chain_tree, free_body, pendulum, random_tree
+from kin_trees import (chain_tree, free_body, mixed_tree, multi_joint_tree, pendulum, random_tree,
+                       slider, spherical_pendulum, two_joint_body)
 from osc_amd.kinematics import KinematicsBatch, load_tree, random_states
 
 pytestmark = pytest.mark.gpu
@@ -29,23 +30,45 @@ def _mjcf_tree(robot):
     return load_mjcf_robot(robot, os.path.join(os.path.dirname(kin_json_path(robot)), f"{robot}.xml"))
 
 
+def _split(tree):
+    """A tree with MuJoCo joint lists through the MJCF reader: one joint per body (chains)."""
+    import os
+    import tempfile
+    from osc_amd.mjcf import load_mjcf, tree_to_mjcf
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "m.xml")
+        with open(path, "w") as fh:
+            fh.write(tree_to_mjcf(tree))
+        bn = [tree["bodies"][s["body"]].get("name", f"b{s['body']}") for s in tree["sites"]]
+        sn = [s.get("name", f"s{k}") for k, s in enumerate(tree["sites"])]
+        return load_mjcf(path, bn, sn)
+
+
+def _dfs(tree):
+    from test_mjcf import _dfs as dfs
+    return dfs(tree)
+
+
 def _trees():
     return {"unitree_go2": load_tree("unitree_go2"), "walter_sr": load_tree("walter_sr"),
             "random_free": random_tree(5), "random_fixed": random_tree(6, free_root=False),
             "chain16": chain_tree(7), "unitree_go2_mjcf": _mjcf_tree("unitree_go2"),
-            "walter_sr_mjcf": _mjcf_tree("walter_sr")}
+            "walter_sr_mjcf": _mjcf_tree("walter_sr"),
+            "slide_ball_free": mixed_tree(2), "slide_ball_fixed": mixed_tree(3, free_root=False)}
 
 
 TREES = _trees()
 
 
-def _check(tree, nenv, seed, base_pos_zero=True):
+def _check(tree, nenv, seed, base_pos_zero=True, oracle_tree=None):
+    """Kernel on `tree` against the oracle on `oracle_tree` (default: the same tree; a tree with
+    joint lists for a split descriptor)."""
     kb = KinematicsBatch(tree=tree)
     qpos, qvel = random_states(tree, nenv, seed, base_pos_zero=base_pos_zero)
     out = kb.compute(qpos, qvel)
     torch.cuda.synchronize()
     M, C, J, b, X = (t.cpu().numpy() for t in (out.M, out.C, out.J, out.b, out.site_xpos))
-    m = kin.KinModel(tree)
+    m = kin.KinModel(oracle_tree or tree)
     for e in range(nenv):
         Mr, Cr, Jr, br = kin.kinematics(m, qpos[e], qvel[e])
         Xr = kin.site_positions(m, qpos[e])
@@ -205,3 +228,59 @@ def test_known_answer_trees(gpu):
         Mk, Ck = free_body_known_answer(q[e], qvel[e, :3], qvel[e, 3:])
         np.testing.assert_allclose(out.M[e].cpu().numpy(), Mk, atol=1e-14)
         np.testing.assert_allclose(out.C[e].cpu().numpy(), Ck, atol=1e-13)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_multi_joint_bodies_match_oracle(gpu, seed):
+    """Bodies with MuJoCo joint lists (hinge / slide pairs and triples, hinge-then-ball): the
+    MJCF reader's chain descriptor on the GPU against the oracle restating the lists directly."""
+    tree = _dfs(multi_joint_tree(seed))
+    _check(_split(tree), 37, 300 + seed, oracle_tree=tree)
+
+
+def test_known_answer_slide_ball_two_joint(gpu):
+    """The kernel against closed forms (tests/test_kinematics_oracle.py): a slider (M = m +
+    armature, qfrc_bias = -m g.a, Jp = a), a spherical pendulum (ball: M = I_O, qfrc_bias =
+    w x I_O w - l x R'm g, Jp = -R[l]x, Jr = R) and a two-hinge body split by the MJCF reader."""
+    from test_kinematics_oracle import spherical_known_answer, two_joint_known_answer
+    t = slider()
+    a = np.asarray(t["bodies"][0]["axis"]) / np.linalg.norm(t["bodies"][0]["axis"])
+    kb = KinematicsBatch(tree=t)
+    q = np.array([[0.2], [-0.4]])
+    out = kb.compute(q, np.array([[-1.0], [2.5]]))
+    torch.cuda.synchronize()
+    for e in range(2):
+        assert abs(out.M[e, 0, 0].item() - 1.32) <= 1e-14
+        assert abs(out.C[e, 0].item() - 1.3 * 9.81 * a[2]) <= 1e-13
+        np.testing.assert_allclose(out.J[e, :3, 0].cpu().numpy(), a, atol=1e-15)
+        np.testing.assert_allclose(out.J[e, 3:, 0].cpu().numpy(), 0.0, atol=0)
+        np.testing.assert_allclose(out.b[e].cpu().numpy(), 0.0, atol=1e-15)
+        np.testing.assert_allclose(out.site_xpos[e, 0].cpu().numpy(),
+                                   np.array([0.1, 0.2, 0.3]) + a * q[e, 0], atol=1e-15)
+    kb = KinematicsBatch(tree=spherical_pendulum())
+    rng = np.random.default_rng(21)
+    qq = rng.normal(size=(5, 4))
+    qq /= np.linalg.norm(qq, axis=1, keepdims=True)
+    wb = rng.normal(size=(5, 3))
+    out = kb.compute(qq, wb)
+    torch.cuda.synchronize()
+    for e in range(5):
+        Mk, Ck, Jp, Jr, bp = spherical_known_answer(qq[e], wb[e])
+        np.testing.assert_allclose(out.M[e].cpu().numpy(), Mk, atol=1e-15)
+        np.testing.assert_allclose(out.C[e].cpu().numpy(), Ck, atol=1e-14)
+        np.testing.assert_allclose(out.J[e, :3].cpu().numpy(), Jp, atol=1e-15)
+        np.testing.assert_allclose(out.J[e, 3:].cpu().numpy(), Jr, atol=1e-15)
+        np.testing.assert_allclose(out.b[e, :3].cpu().numpy(), bp, atol=1e-14)
+    kb = KinematicsBatch(tree=_split(two_joint_body()))
+    th = np.array([[0.3, -0.5], [1.2, 0.9], [-2.2, 2.8]])
+    thd = np.array([[1.1, -0.7], [-2.0, 0.4], [0.3, 1.9]])
+    out = kb.compute(th, thd)
+    torch.cuda.synchronize()
+    for e in range(3):
+        Mk, Ck, Jp, Jr, bp, br = two_joint_known_answer(*th[e], *thd[e])
+        np.testing.assert_allclose(out.M[e].cpu().numpy(), Mk, atol=1e-15)
+        np.testing.assert_allclose(out.C[e].cpu().numpy(), Ck, atol=1e-13)
+        np.testing.assert_allclose(out.J[e, :3].cpu().numpy(), Jp, atol=1e-15)
+        np.testing.assert_allclose(out.J[e, 3:].cpu().numpy(), Jr, atol=1e-15)
+        np.testing.assert_allclose(out.b[e, :3].cpu().numpy(), bp, atol=1e-14)
+        np.testing.assert_allclose(out.b[e, 3:].cpu().numpy(), br, atol=1e-15)

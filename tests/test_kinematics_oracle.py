@@ -15,9 +15,11 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "oracle"))
 import kinematics as kin  # noqa: E402
-from kin_trees import chain_tree, free_body, pendulum, random_tree  # noqa: E402
+from kin_trees import (chain_tree, free_body, mixed_tree, multi_joint_tree, pendulum,  # noqa: E402
+                       random_tree, slider, spherical_pendulum, two_joint_body)
 
-ROBOTS = ["unitree_go2", "walter_sr", "random_free", "random_fixed", "chain"]
+ROBOTS = ["unitree_go2", "walter_sr", "random_free", "random_fixed", "chain", "mixed",
+          "mixed_fixed", "multi_joint"]
 EPS = 1e-6
 
 
@@ -28,6 +30,12 @@ def _load(name):
         return kin.KinModel(random_tree(6, free_root=False))
     if name == "chain":
         return kin.KinModel(chain_tree(7))
+    if name == "mixed":
+        return kin.KinModel(mixed_tree(8))
+    if name == "mixed_fixed":
+        return kin.KinModel(mixed_tree(9, free_root=False))
+    if name == "multi_joint":
+        return kin.KinModel(multi_joint_tree(10))
     return kin.load(name)
 
 
@@ -174,3 +182,86 @@ def test_free_body_known_answer():
         np.testing.assert_allclose(J[:3], np.hstack([np.eye(3), np.zeros((3, 3))]), atol=1e-15)
         np.testing.assert_allclose(J[3:], np.hstack([np.zeros((3, 3)), R]), atol=1e-15)
         np.testing.assert_allclose(b, 0.0, atol=1e-14)   # origin = COM: no bias acceleration
+
+
+def test_slide_known_answer():
+    """A mass on a slide along the unit axis a: x = x0 + a q, M = m + armature, qfrc_bias =
+    -m g.a, Jp = a, Jr = 0, no bias acceleration."""
+    t = slider()
+    m = kin.KinModel(t)
+    a = np.asarray(t["bodies"][0]["axis"]) / np.linalg.norm(t["bodies"][0]["axis"])
+    for q, qd in ((0.2, -1.0), (-0.4, 2.5)):
+        M, C, J, b = kin.kinematics(m, np.array([q]), np.array([qd]))
+        np.testing.assert_allclose(kin.site_positions(m, [q])[0], np.array([0.1, 0.2, 0.3]) + a * q,
+                                   atol=1e-15)
+        np.testing.assert_allclose(M[0, 0], 1.3 + 0.02, rtol=1e-14)
+        np.testing.assert_allclose(C[0], 1.3 * 9.81 * a[2], rtol=1e-14)
+        np.testing.assert_allclose(J[:3, 0], a, atol=1e-15)
+        np.testing.assert_allclose(J[3:, 0], 0.0, atol=0)
+        np.testing.assert_allclose(b, 0.0, atol=1e-15)
+
+
+def spherical_known_answer(quat, wb, mass=0.8, length=0.5, i_small=1e-4, g=9.81):
+    """Ball joint at the origin, point-like mass at l = (0, 0, -L) in the body frame; dofs = the
+    body-frame angular velocity.  M = I_O (inertia about the anchor, body frame); qfrc_bias =
+    w x I_O w - l x (R' m g); Jp = -R [l]x, Jr = R; tip acceleration w x (w x p)."""
+    R = kin.quat2mat(quat)
+    lv = np.array([0.0, 0.0, -length])
+    IO = np.diag([mass * length ** 2 + i_small, mass * length ** 2 + i_small, i_small])
+    gv = np.array([0.0, 0.0, -g])
+    C = np.cross(wb, IO @ wb) - np.cross(lv, R.T @ (mass * gv))
+    lx = np.array([[0, -lv[2], lv[1]], [lv[2], 0, -lv[0]], [-lv[1], lv[0], 0]])
+    Jp = -R @ lx
+    w = R @ wb
+    p = R @ lv
+    return IO, C, Jp, R, np.cross(w, np.cross(w, p))
+
+
+def test_ball_known_answer():
+    m = kin.KinModel(spherical_pendulum())
+    rng = np.random.default_rng(21)
+    for _ in range(3):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        wb = rng.normal(size=3)
+        M, C, J, b = kin.kinematics(m, q, wb)
+        Mk, Ck, Jp, Jr, bp = spherical_known_answer(q, wb)
+        np.testing.assert_allclose(M, Mk, atol=1e-15)
+        np.testing.assert_allclose(C, Ck, atol=1e-14)
+        np.testing.assert_allclose(J[:3], Jp, atol=1e-15)
+        np.testing.assert_allclose(J[3:], Jr, atol=1e-15)
+        np.testing.assert_allclose(b[:3], bp, atol=1e-14)
+        np.testing.assert_allclose(b[3:], 0.0, atol=1e-15)
+
+
+def two_joint_known_answer(t1, t2, d1, d2, mass=1.1, length=0.6, i_small=1e-4, arm=(0.01, 0.03),
+                           g=9.81):
+    """Hinge about x (t1) then about the rotated y (t2) on ONE body, point mass at -L z:
+    p = (-L s2, L c2 s1, -L c2 c1), M = diag(m L^2 c2^2 + i + a1, m L^2 + i + a2),
+    qfrc_bias = m g L (c2 s1, s2 c1) + m L^2 c2 s2 (-2 d1 d2, d1^2)."""
+    L = length
+    s1, c1, s2, c2 = np.sin(t1), np.cos(t1), np.sin(t2), np.cos(t2)
+    M = np.diag([mass * L * L * c2 * c2 + i_small + arm[0], mass * L * L + i_small + arm[1]])
+    C = mass * g * L * np.array([c2 * s1, s2 * c1]) + \
+        mass * L * L * c2 * s2 * np.array([-2 * d1 * d2, d1 * d1])
+    Jp = np.array([[0.0, -L * c2], [L * c2 * c1, -L * s2 * s1], [L * c2 * s1, L * s2 * c1]])
+    Jr = np.array([[1.0, 0.0], [0.0, c1], [0.0, s1]])
+    ss = d1 * d1 + d2 * d2
+    bp = np.array([L * s2 * d2 * d2, -L * (c2 * s1 * ss + 2 * s2 * c1 * d1 * d2),
+                   L * (c2 * c1 * ss - 2 * s2 * s1 * d1 * d2)])
+    br = d1 * d2 * np.array([0.0, -s1, c1])
+    return M, C, Jp, Jr, bp, br
+
+
+def test_two_joint_body_known_answer():
+    m = kin.KinModel(two_joint_body())
+    assert (m.nq, m.nv, m.njnt) == (2, 2, 2)
+    for t1, t2, d1, d2 in ((0.3, -0.5, 1.1, -0.7), (1.2, 0.9, -2.0, 0.4), (-2.2, 2.8, 0.3, 1.9)):
+        M, C, J, b = kin.kinematics(m, np.array([t1, t2]), np.array([d1, d2]))
+        Mk, Ck, Jp, Jr, bp, br = two_joint_known_answer(t1, t2, d1, d2)
+        np.testing.assert_allclose(M, Mk, atol=1e-15)
+        np.testing.assert_allclose(C, Ck, atol=1e-13)
+        np.testing.assert_allclose(J[:3], Jp, atol=1e-15)
+        np.testing.assert_allclose(J[3:], Jr, atol=1e-15)
+        np.testing.assert_allclose(b[:3], bp, atol=1e-14)
+        np.testing.assert_allclose(b[3:], br, atol=1e-15)

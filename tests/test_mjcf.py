@@ -24,7 +24,8 @@ from osc_amd import _lib
 from osc_amd.mjcf import load_mjcf, load_mjcf_robot, tree_to_mjcf
 
 import kinematics as kin   # oracle (checker only)
-from kin_trees import chain_tree, free_body, pendulum, random_tree
+from kin_trees import (chain_tree, free_body, mixed_tree, multi_joint_tree, pendulum, random_tree,
+                       slider, spherical_pendulum, two_joint_body)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CFG = os.path.join(REPO, "operational-space-control_amd", "config")
@@ -59,10 +60,10 @@ def _desc_equal(a, b, exact=True):
             if k in ("quat", "iquat"):                 # MuJoCo normalises quaternions
                 y = y / np.linalg.norm(y, axis=1, keepdims=True)
             assert np.allclose(x, y, rtol=0, atol=1e-15), k
-    hinge = [i for i, v in enumerate(a["bodies"]) if v["joint"] == "hinge"]
-    for k in ("axis", "jnt_pos"):
-        x = np.array([a["bodies"][i][k] for i in hinge], dtype=float)
-        y = np.array([b["bodies"][i][k] for i in hinge], dtype=float)
+    for k, types in (("axis", ("hinge", "slide")), ("jnt_pos", ("hinge", "ball"))):
+        idx = [i for i, v in enumerate(a["bodies"]) if v["joint"] in types]
+        x = np.array([a["bodies"][i][k] for i in idx], dtype=float)
+        y = np.array([b["bodies"][i][k] for i in idx], dtype=float)
         assert np.array_equal(x, y), k
     assert [s["body"] for s in a["sites"]] == [s["body"] for s in b["sites"]]
     assert np.array_equal(np.array([s["pos"] for s in a["sites"]], dtype=float),
@@ -275,16 +276,30 @@ def test_radian_and_eulerseq(tmp_path):
 
 
 @pytest.mark.parametrize("text,why", [
-    ("<mujoco><worldbody><body name='a'><joint/><geom size='1'/></body></worldbody></mujoco>",
-     "inertia from geoms"),
-    ("<mujoco><worldbody><body name='a'><joint type='slide'/><inertial pos='0 0 0' mass='1' "
-     "diaginertia='1 1 1'/></body></worldbody></mujoco>", "slide joint"),
-    ("<mujoco><worldbody><body name='a'><joint/><joint/><inertial pos='0 0 0' mass='1' "
-     "diaginertia='1 1 1'/></body></worldbody></mujoco>", "two joints"),
+    ("<mujoco><worldbody><body name='a'><joint/><geom type='mesh' mesh='m'/></body></worldbody>"
+     "</mujoco>", "inertia from a mesh geom"),
+    ("<mujoco><compiler inertiafromgeom='true'/><worldbody><body name='a'><joint/><inertial "
+     "pos='0 0 0' mass='1' diaginertia='1 1 1'/><geom type='mesh' mesh='m'/></body></worldbody>"
+     "</mujoco>", "mesh geom used under inertiafromgeom true"),
+    ("<mujoco><worldbody><body name='a'><joint type='ball'/><joint/><inertial pos='0 0 0' "
+     "mass='1' diaginertia='1 1 1'/></body></worldbody></mujoco>", "ball then hinge"),
+    ("<mujoco><worldbody><body name='a'><freejoint/><joint/><inertial pos='0 0 0' mass='1' "
+     "diaginertia='1 1 1'/></body></worldbody></mujoco>", "free joint with another joint"),
+    ("<mujoco><worldbody><body name='a'><joint ref='0.3'/><inertial pos='0 0 0' mass='1' "
+     "diaginertia='1 1 1'/></body></worldbody></mujoco>", "joint ref"),
+    ("<mujoco><default><joint ref='5'/></default><worldbody><body name='a'><joint/><inertial "
+     "pos='0 0 0' mass='1' diaginertia='1 1 1'/></body></worldbody></mujoco>", "default ref"),
+    ("<mujoco><worldbody><body name='a'><joint type='screw'/><inertial pos='0 0 0' mass='1' "
+     "diaginertia='1 1 1'/></body></worldbody></mujoco>", "unknown joint type"),
+    ("<mujoco><compiler settotalmass='5'/><worldbody><body name='a'><joint/><inertial "
+     "pos='0 0 0' mass='1' diaginertia='1 1 1'/></body></worldbody></mujoco>", "settotalmass"),
+    ("<mujoco><worldbody><body name='a'><joint/><geom type='plane' size='1 1 1'/></body>"
+     "</worldbody></mujoco>", "plane in a body"),
     ("<mujoco><worldbody><body name='a' class='nope'><joint class='nope'/><inertial pos='0 0 0' "
      "mass='1' diaginertia='1 1 1'/></body></worldbody></mujoco>", "unknown class"),
     ("<mujoco><worldbody><body name='a'><joint/>", "unterminated"),
-    ("<mujoco><include file='x.xml'/><worldbody/></mujoco>", "include"),
+    ("<mujoco><include file='no_such_file.xml'/><worldbody/></mujoco>", "missing include"),
+    ("<mujoco><include file='e.xml'/><worldbody/></mujoco>", "include cycle"),
     ("<mujoco><worldbody><site name='s'/><body name='a'><joint/><inertial pos='0 0 0' mass='1' "
      "diaginertia='1 1 1'/></body></worldbody></mujoco>", "world site as task site"),
     ("<mujoco><worldbody><body name='a'><joint/><inertial pos='0 0 0' mass='1' "
@@ -305,3 +320,169 @@ def test_missing_file_and_bad_args(tmp_path):
     with pytest.raises(_lib.OSCError) as e:
         load_mjcf_robot("no_such_robot", os.path.join(CFG, "unitree_go2.xml"))
     assert e.value.code == 1
+
+
+# ---------------------------------------------------------------- widened dialect
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_slide_and_ball_trees_roundtrip(tmp_path, seed):
+    """Trees mixing slide, ball and hinge joints through the MJCF door: same descriptor (up to
+    welded-body fusion) and the oracle's M, C, J, b unchanged."""
+    tree = _dfs(mixed_tree(seed))
+    path = _write(tmp_path, "m.xml", tree_to_mjcf(tree))
+    bn, sn = _names(tree)
+    got = load_mjcf(path, bn, sn)
+    assert {b["joint"] for b in got["bodies"]} >= {"slide", "ball"}
+    _kin_close(got, tree)
+
+
+@pytest.mark.parametrize("tree", [slider(), spherical_pendulum()], ids=["slider", "ball"])
+def test_slide_ball_known_trees_roundtrip(tmp_path, tree):
+    path = _write(tmp_path, "m.xml", tree_to_mjcf(tree))
+    bn, sn = _names(tree)
+    got = load_mjcf(path, bn, sn)
+    _desc_equal(got, tree, exact=False)
+    _kin_close(got, tree)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_multi_joint_bodies_split_into_chains(tmp_path, seed):
+    """Bodies with several joints (MuJoCo applies them in order) become chains of one-joint
+    bodies, the leading ones massless at zero offset; names resolve to the chain's last body.
+    The oracle restates the joint lists directly: its M, C, J, b of the split descriptor equal
+    those of the original tree."""
+    tree = _dfs(multi_joint_tree(seed))
+    path = _write(tmp_path, "m.xml", tree_to_mjcf(tree))
+    bn, sn = _names(tree)
+    got = load_mjcf(path, bn, sn)
+    njoint = sum(len(b.get("joints", [])) + (b.get("joint", "none") != "none")
+                 for b in tree["bodies"])
+    assert sum(b["joint"] != "none" for b in got["bodies"]) == njoint
+    massless = [i for i, b in enumerate(got["bodies"]) if b["mass"] == 0.0]
+    assert len(massless) == sum(max(len(b.get("joints", [])) - 1, 0) for b in tree["bodies"])
+    links = [b for b in got["bodies"] if b["parent"] in massless]   # 2nd..last joint of a body
+    assert len(links) == len(massless)
+    assert all(b["pos"] == [0.0, 0.0, 0.0] and b["quat"] == [1.0, 0.0, 0.0, 0.0] for b in links)
+    _kin_close(got, tree, n=4)
+
+
+def test_two_joint_body_known_answer_through_mjcf(tmp_path):
+    tree = two_joint_body()
+    got = load_mjcf(_write(tmp_path, "u.xml", tree_to_mjcf(tree)), ["u"], ["tip"])
+    assert [b["joint"] for b in got["bodies"]] == ["hinge", "hinge"]
+    assert [b["parent"] for b in got["bodies"]] == [-1, 0]
+    assert got["bodies"][0]["mass"] == 0.0 and got["bodies"][1]["mass"] == 1.1
+    assert got["sites"][0]["body"] == 1 and got["sites"][0]["jac_body"] == 1
+    _kin_close(got, tree)
+
+
+def _tensor(b):
+    R = kin.quat2mat(b["iquat"])
+    return R @ np.diag(b["diaginertia"]) @ R.T
+
+
+GEOM_CASES = {
+    # type, attributes, (mass, com, inertia tensor about the COM in the body frame)
+    "sphere": ("<geom type='sphere' size='0.1' pos='0.1 0 0' density='500'/>",
+               lambda: (500 * 4 / 3 * np.pi * 1e-3, [0.1, 0, 0],
+                        np.eye(3) * 0.4 * 0.01 * 500 * 4 / 3 * np.pi * 1e-3)),
+    "box": ("<geom type='box' size='0.1 0.2 0.3' mass='2' euler='0 0 90'/>",
+            # box axes x, y -> body y, -x: body I_xx = the box's I_yy and vice versa
+            lambda: (2.0, [0, 0, 0],
+                     np.diag([2 * (0.01 + 0.09) / 3, 2 * (0.04 + 0.09) / 3,
+                              2 * (0.04 + 0.01) / 3]))),
+    "cylinder": ("<geom type='cylinder' fromto='0 0 0 0 0 0.4' size='0.05' mass='1.5'/>",
+                 lambda: (1.5, [0, 0, 0.2],
+                          np.diag([1.5 * (3 * 0.0025 + 0.16) / 12, 1.5 * (3 * 0.0025 + 0.16) / 12,
+                                   1.5 * 0.0025 / 2]))),
+    "capsule_x": ("<geom type='capsule' fromto='0 0 0 0.4 0 0' size='0.05'/>",
+                  None),   # closed form below
+    "ellipsoid": ("<geom type='ellipsoid' size='0.1 0.2 0.3' mass='3'/>",
+                  lambda: (3.0, [0, 0, 0], np.diag([3 * (0.04 + 0.09) / 5, 3 * (0.01 + 0.09) / 5,
+                                                    3 * (0.01 + 0.04) / 5]))),
+}
+
+
+def _capsule(r, h, rho=1000.0):
+    """Capsule along z, radius r, half-length h: cylinder plus two hemispheres (each's COM at
+    3r/8 from its flat face), density rho."""
+    vc, vs = np.pi * r * r * 2 * h, 4 / 3 * np.pi * r ** 3
+    Ic = rho * vc * (3 * r * r + 4 * h * h) / 12
+    # hemispheres about the capsule centre: 2 x [2/5 (m/2) r^2 - (m/2)(3r/8)^2 + (m/2)(h + 3r/8)^2]
+    ms = rho * vs
+    Is = 2 * (0.4 * ms / 2 * r * r - ms / 2 * (3 * r / 8) ** 2 + ms / 2 * (h + 3 * r / 8) ** 2)
+    return rho * (vc + vs), Ic + Is, rho * vc * r * r / 2 + 0.4 * ms * r * r
+
+
+@pytest.mark.parametrize("case", sorted(GEOM_CASES))
+def test_inertia_from_primitive_geoms_closed_form(tmp_path, case):
+    geom, ref = GEOM_CASES[case]
+    text = f"""<mujoco><worldbody><body name="a"><joint type="hinge"/>{geom}<site name="s"/>
+      </body></worldbody></mujoco>"""
+    d = load_mjcf(_write(tmp_path, "g.xml", text), ["a"], ["s"])
+    b = d["bodies"][0]
+    if ref is None:
+        m, Ixx, Izz = _capsule(0.05, 0.2)
+        mass, com, I = m, [0.2, 0, 0], np.diag([Izz, Ixx, Ixx])   # axis along body x
+    else:
+        mass, com, I = ref()
+    assert abs(b["mass"] - mass) <= 1e-12 * mass
+    np.testing.assert_allclose(b["ipos"], com, atol=1e-15)
+    np.testing.assert_allclose(_tensor(b), I, atol=1e-14 * np.abs(I).max())
+
+
+def test_inertia_from_several_geoms_and_modes(tmp_path):
+    """Two spheres combine about their joint COM (parallel axes); a group outside
+    inertiagrouprange is ignored; <inertial> wins under auto, geoms win under true, neither
+    under false (massless body)."""
+    def model(compiler, inertial):
+        return f"""<mujoco><compiler {compiler}/><worldbody><body name="a"><joint/>
+          {inertial}
+          <geom type="sphere" size="0.1" pos="0.2 0 0" mass="1"/>
+          <geom type="sphere" size="0.1" pos="-0.2 0 0" mass="3"/>
+          <geom type="box" size="1 1 1" mass="100" group="3"/>
+          <site name="s"/></body></worldbody></mujoco>"""
+    inert = '<inertial pos="0 0 0" mass="7" diaginertia="1 2 3"/>'
+    I1 = 0.4 * 0.01
+    want = np.diag([4 * I1, 4 * I1 + 0.04 * 4 - 4 * 0.1 ** 2, 4 * I1 + 0.04 * 4 - 4 * 0.1 ** 2])
+    for comp, ine, exp in (('inertiagrouprange="0 2"', "", "geoms"),
+                           ('inertiafromgeom="auto" inertiagrouprange="0 2"', inert, "inertial"),
+                           ('inertiafromgeom="true" inertiagrouprange="0 2"', inert, "geoms"),
+                           ('inertiafromgeom="false"', "", "none"),
+                           ('', "", "all")):
+        b = load_mjcf(_write(tmp_path, "m.xml", model(comp, ine)), ["a"], ["s"])["bodies"][0]
+        if exp == "geoms":
+            assert abs(b["mass"] - 4.0) < 1e-14
+            np.testing.assert_allclose(b["ipos"], [-0.1, 0, 0], atol=1e-15)
+            np.testing.assert_allclose(_tensor(b), want, atol=1e-14)
+        elif exp == "inertial":
+            assert b["mass"] == 7.0 and b["diaginertia"] == [1.0, 2.0, 3.0]
+        elif exp == "none":
+            assert b["mass"] == 0.0
+        else:   # default range 0..5 keeps the group-3 box
+            assert abs(b["mass"] - 104.0) < 1e-12
+
+
+def test_include_files_relative_to_the_model(tmp_path):
+    """<include file> splices the included <mujoco>'s children in place, anywhere in the tree,
+    relative to the main file's directory, nested includes too."""
+    sub = tmp_path / "parts"
+    sub.mkdir()
+    (sub / "defaults.xml").write_text(
+        '<mujoco><default><joint axis="0 1 0" armature="0.02"/></default></mujoco>')
+    (sub / "leg.xml").write_text(
+        '<mujoco><body name="leg" pos="0 0 -0.3"><joint/><inertial pos="0 0 -0.1" mass="0.5" '
+        'diaginertia="0.01 0.01 0.001"/><include file="parts/foot.xml"/></body></mujoco>')
+    (sub / "foot.xml").write_text('<mujoco><site name="foot" pos="0 0 -0.2"/></mujoco>')
+    main = """<mujoco><include file="parts/defaults.xml"/><worldbody>
+      <body name="base"><freejoint/><inertial pos="0 0 0" mass="3" diaginertia="0.1 0.1 0.1"/>
+      <include file="parts/leg.xml"/></body></worldbody></mujoco>"""
+    inline = """<mujoco><default><joint axis="0 1 0" armature="0.02"/></default><worldbody>
+      <body name="base"><freejoint/><inertial pos="0 0 0" mass="3" diaginertia="0.1 0.1 0.1"/>
+      <body name="leg" pos="0 0 -0.3"><joint/><inertial pos="0 0 -0.1" mass="0.5"
+      diaginertia="0.01 0.01 0.001"/><site name="foot" pos="0 0 -0.2"/></body></body>
+      </worldbody></mujoco>"""
+    a = load_mjcf(_write(tmp_path, "main.xml", main), ["leg"], ["foot"])
+    b = load_mjcf(_write(tmp_path, "inline.xml", inline), ["leg"], ["foot"])
+    _desc_equal(a, b)
+    assert a["bodies"][1]["axis"] == [0.0, 1.0, 0.0] and a["bodies"][1]["armature"] == 0.02
