@@ -90,15 +90,21 @@ int osc_kin_desc_from_json(const char* robot, const char* json_path, osc_kin_des
 
 /* Host-only: fill `desc` from a MuJoCo MJCF file -- the reference's xml_path, which its
  * controller loads with mj_loadXML (operational_space_controller.h:114-152).  The subset of
- * MJCF that update_osc_data's quantities depend on is read: <compiler angle eulerseq>,
- * <option gravity>, nested <default> classes (joint / site attributes, childclass / class),
- * <body pos + quat | euler | axisangle | xyaxes | zaxis>, <inertial pos, orientation, mass,
- * diaginertia | fullinertia>, <joint type="hinge" | "free" axis pos armature>, <freejoint>,
- * <site pos>.  Geoms, actuators, sensors, contacts, visual/asset sections are skipped (they do
- * not enter M, C, J, b).  Bodies are numbered in MuJoCo's depth-first order; sites likewise.
- * Errors (OSC_ERR_IO): unreadable or malformed XML, a body without <inertial> (MuJoCo would
- * infer it from geoms), slide / ball joints, more than one joint on a body, <include>/<frame>,
- * unknown names.
+ * MJCF that update_osc_data's quantities depend on is read: <compiler angle eulerseq
+ * inertiafromgeom inertiagrouprange>, <option gravity>, nested <default> classes (childclass /
+ * class), <include file> (anywhere, relative to the main file, nested), <body pos + quat | euler |
+ * axisangle | xyaxes | zaxis>, <inertial pos, orientation, mass, diaginertia | fullinertia>,
+ * inertia from primitive geoms (sphere, capsule, cylinder, box, ellipsoid; mass | density; pos +
+ * orientation | fromto) under inertiafromgeom auto (default: bodies without <inertial>) / true,
+ * <joint type="free" | "ball" | "slide" | "hinge" axis pos armature> -- several per body, applied
+ * in order (the body becomes a chain of one-joint bodies) -- <freejoint>, <site pos | fromto>.
+ * Actuators, sensors, contacts, visual/asset sections are skipped (they do not enter M, C, J, b).
+ * Bodies are numbered in MuJoCo's depth-first order; sites likewise.
+ * Errors (OSC_ERR_IO): unreadable or malformed XML (or included file), mesh / sdf / hfield geoms
+ * that would give a body its inertia, a plane geom in a moving body, a non-zero joint ref,
+ * compiler settotalmass / boundmass / boundinertia, a ball joint followed by a rotating joint on
+ * the same body, a free joint not alone on a top-level body, <frame> / <replicate> /
+ * <composite>, unknown names.
  * Task sites: task site k = (point, Jacobian body) with Jacobian body = body_names[k] and
  *   site_order OSC_MJCF_SITES_BY_NAME:     point = the site named site_names[k]
  *                                          (walter_sr: site_xpos(site_ids), W/osc.h:417);
