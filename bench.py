@@ -559,8 +559,13 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
     achieved = bps * nenv / (ipm_ms * 1e-3) / 1e9
     achieved_pair = bps * nenv / (kernel_ms * 1e-3) / 1e9
     traffic = traffic_pair = None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as fh:
+    tpath = args.traffic_json
+    if not os.path.exists(tpath) or json.load(open(tpath)).get("nenv") != nenv:
+        # PMC passes at other batch sizes sit beside it (tools/pmc_summary.py)
+        alt = os.path.join(os.path.dirname(tpath), f"pmc_traffic_{nenv}.json")
+        tpath = alt if os.path.exists(alt) else tpath
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
             tj = json.load(fh)
         if tj.get("robot") == args.robot and tj.get("nenv") == nenv:
             traffic_pair = tj.get("bytes_per_launch")

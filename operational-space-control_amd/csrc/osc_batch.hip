@@ -1226,8 +1226,9 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // holds column l in c0 and column l+16 in c1.  Right-looking; at step k every lane j > k
 // applies  c_j[i] -= L[i][k] L[j][k] D_k  for i > k with the pivot column entry c_k[i]
 // broadcast by DPP straight into the FMA.  On exit (for slot column j):
-//   c[i], i > j : L[i][j] * D[j]     (column j of L, unscaled)
-//   c[i], i < j : L[j][i] * D[i]     (row j of L, scaled -- left by the symmetric update)
+//   c[i], i > j : -L[i][j] D[j] / D[i]  (column j of L, unscaled, times -1/D_i: backward solve)
+//   c[i], i < j : -L[j][i]              (row j of L: forward solve)
+//   c[j]        : -1
 //   dinv0, dinv1: 1 / D[j]
 // thr0, thr1: 1e-13 x the original diagonal (Cholesky-infinity test: a pivot not above it
 // becomes 1e128).  sdinv: 2 x 16 doubles of LDS for this row: every lane writes 1/D_k at step k
@@ -1249,11 +1250,16 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
     const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
     const double inv = recip1(dk);
     sdinv[k] = inv;
+    // Row k of every column, scaled by -1/D_k once here, is all the triangular solves read of
+    // it: lanes j > k hold L[j][k] D_k -> -L[j][k] (forward), lanes j < k hold L[k][j] D_j ->
+    // -L[k][j] D_j / D_k (backward, D-scaled), so neither solve multiplies inside its chain.
+    c0[k] = -c0[k] * inv;
+    c1[k] = -c1[k] * inv;
     // -L[lane][k] for the lanes still to be eliminated (slot 0: lane > k; slot 1: lane+16 > k,
     // which holds for every slot-1 lane -- padding mirrors included -- while k < 16)
-    const double t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(-c0[k] * inv);
+    const double t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(c0[k]);
     constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
-    const double t1 = keep_lanes<rows_mask(kT1)>(-c1[k] * inv);
+    const double t1 = keep_lanes<rows_mask(kT1)>(c1[k]);
     static_for<k + 1, N>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (s == 0) {
@@ -1271,9 +1277,15 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
 
 // Solve K x = r with the factor above; r0 (var l), r1 (var l+16) in, x out.  Every lane of
 // the row is updated at every step (no lane masks): a lane whose value is already final saves
-// it at its own pivot step and may take garbage afterwards.
-//   forward   z = L^-1 r             a_j += (-z_k / D_k) * (L[j][k] D_k)
-//   backward  in D-scaled form       a_j = z_j - sum_{k>j} (L[k][j] D_j) x_k,  x_j = a_j / D_j
+// it at its own pivot step and may take garbage afterwards.  The factor's row k is pre-scaled
+// by -1/D_k (ldl_rows), so each step is the pivot's broadcast straight into the FMAs -- no
+// multiply in the dependency chain (Go2 4,096: 0.183 -> 0.178 ms per solve;
+// profiles/r03_ab_ldl_prescale.txt):
+//   forward   z = L^-1 r             a_j += a_k * (-L[j][k])
+//   backward  in D-scaled form       a_j += a_k * (-L[k][j] D_j / D_k),  x_j = a_j / D_j
+// The other slot's FMA goes first: the own slot's FMA rewrites the pivot lane (c[k] = -1 there).
+// (Masking each FMA to the lanes it may change through EXEC instead of saving was measured
+// slower: 0.186 ms -- the EXEC writes cost more than the two v_cndmask they replace.)
 // (ldl_fwd_rows / ldl_bwd_rows: the two halves, for callers that act on z in between.)
 template <int N>
 __device__ __forceinline__ void ldl_fwd_rows(const double (&c0)[N], const double (&c1)[N],
@@ -1284,16 +1296,16 @@ __device__ __forceinline__ void ldl_fwd_rows(const double (&c0)[N], const double
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
     constexpr unsigned long long kPiv = rows_mask(1u << kl);
-    double zv;
     if constexpr (s == 0) {
-      zv = -a0 * dinv0;
       z0 = select_lanes<kPiv>(a0, z0);
+      const double p = a0;
+      fmac_bcast<kl, true>(a1, p, c1[k]);
+      if constexpr (k < kRow - 1) fmac_bcast<kl>(a0, p, c0[k]);
     } else {
-      zv = -a1 * dinv1;
       z1 = select_lanes<kPiv>(a1, z1);
+      const double p = a1;
+      fmac_bcast<kl, true>(a1, p, c1[k]);
     }
-    fmac_bcast<kl, true>(a1, zv, c1[k]);
-    if constexpr (k < kRow - 1) fmac_bcast<kl>(a0, zv, c0[k]);
   });
   a0 = z0;
   a1 = z1;
@@ -1302,24 +1314,24 @@ template <int N>
 __device__ __forceinline__ void ldl_bwd_rows(const double (&c0)[N], const double (&c1)[N],
                                              double dinv0, double dinv1,
                                              double& a0, double& a1, int l) {
-  double x0 = 0.0, x1 = 0.0;
+  double x0 = 0.0, x1 = 0.0;                // D-scaled x_j, saved at step j
   static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
     constexpr unsigned long long kPiv = rows_mask(1u << kl);
-    double nxv;
     if constexpr (s == 0) {
-      nxv = -a0 * dinv0;
-      x0 = select_lanes<kPiv>(nxv, x0);
+      x0 = select_lanes<kPiv>(a0, x0);
+      const double p = a0;
+      if constexpr (k >= 1) fmac_bcast<kl, true>(a0, p, c0[k]);
     } else {
-      nxv = -a1 * dinv1;
-      x1 = select_lanes<kPiv>(nxv, x1);
+      x1 = select_lanes<kPiv>(a1, x1);
+      const double p = a1;
+      fmac_bcast<kl, true>(a0, p, c0[k]);
+      if constexpr (k > kRow) fmac_bcast<kl>(a1, p, c1[k]);
     }
-    if constexpr (k >= 1) fmac_bcast<kl, true>(a0, nxv, c0[k]);
-    if constexpr (k > kRow) fmac_bcast<kl, k < 1>(a1, nxv, c1[k]);
   });
-  a0 = -x0;
-  a1 = -x1;
+  a0 = x0 * dinv0;
+  a1 = x1 * dinv1;
 }
 template <int N>
 __device__ __forceinline__ void ldl_solve_rows(const double (&c0)[N], const double (&c1)[N],
@@ -2505,9 +2517,12 @@ __device__ __forceinline__ void ipm_block(
       // (WH: the interior point stops earlier (eps_mu 1e-9, osc_model_create: past that its
       // rotated Newton systems lose accuracy), so the refinement may move y further; it is kept
       // when it has converged -- its last step below 1e-10 of y -- within 0.1 of y)
+      // (WH: both tests against the env's |y| scale, row_max: dlast is a row-wide maximum, and a
+      // lane holding only near-zero variables must not hold it to 1e-10 absolute)
+      const double myr = WHR ? row_max(my) : my;
       const double ok =
           (isfinite(ya0) && isfinite(ya1) &&
-           (WHR ? (mv <= 0.1 * (1.0 + my) && dlast <= 1e-10 * (1.0 + my))
+           (WHR ? (mv <= 0.1 * (1.0 + myr) && dlast <= 1e-10 * (1.0 + myr))
                 : mv <= P->refine_max_move * (1.0 + my))) ? 1.0 : 0.0;
       // (WH: and the wheel rows hold at the refined point)
       double wres = 0.0;
@@ -2525,6 +2540,12 @@ __device__ __forceinline__ void ipm_block(
       // a converged env whose refinement is rejected keeps the interior point's iterate, and says
       // so: it is only as accurate as the interior point's stop
       if (mine && !keep) st = OSC_SOLVE_UNREFINED;
+#ifdef OSC_REFINE_DIAG   // diagnostic builds only: why the refinement was rejected
+      if (mine && !keep)
+        st = OSC_SOLVE_UNREFINED + 16 * (viol_env ? 1 : 0) + 32 * (row_min(ok) == 1.0 ? 0 : 1) +
+             64 * (wres <= ytol ? 0 : 1) + 128 * (row_min(dlast <= 1e-10 * (1.0 + myr) ? 1.0 : 0.0) == 1.0 ? 0 : 1) +
+             256 * (row_min(mv <= 0.1 * (1.0 + myr) ? 1.0 : 0.0) == 1.0 ? 0 : 1);
+#endif
       put_wheel_duals((mine && keep && l < NW) ? sWNu[l] : 0.0);
       wave_sync();
       sVy[j0] = y0;

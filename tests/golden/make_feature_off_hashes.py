@@ -3,11 +3,13 @@
     OSC_LIB_PATH=<libosc_batch.so> python tests/golden/make_feature_off_hashes.py > out.json
 
 Each entry is the SHA-256 of the bytes of (tau, x, status, iters) for one (robot, scenario,
-mask, nenv, seed) batch.  tests/test_gpu_wheels.py checks that the current build reproduces the
-fingerprints made with the round-2 build (the library whose kernels tools/isa_compare.py shows
-unchanged by the variant pruning), i.e. that models without wheel no-slip rows -- the
-feature-off path -- are bitwise what they were.  Regenerate only for an intentional numerical
-change of the default kernels, and say so in the commit.
+mask, nenv, seed) batch.  tests/test_gpu_wheels.py checks that the current build reproduces
+them, i.e. that models without wheel no-slip rows -- the feature-off path -- are bitwise what
+they were.  History: made with the round-2 build; regenerated once in round 3 for the
+intentional change of the LDL factor's storage (row k pre-scaled by -1/D_k, multiply-free
+triangular solves: DESIGN.md §5); the wheel rows' changes since do not reach models without
+them.  Regenerate
+only for an intentional numerical change of the default kernels, and say so in the commit.
 """
 from __future__ import annotations
 

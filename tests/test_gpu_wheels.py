@@ -71,8 +71,8 @@ def _wheel():
 
 def test_feature_off_bitwise_unchanged(gpu):
     """Models without wheel rows -- the feature-off path -- give bitwise the results of the
-    round-2 build (tests/golden/feature_off_hashes.json, made by
-    tests/golden/make_feature_off_hashes.py with that library)."""
+    last intentional numerical change of the default kernels (tests/golden/feature_off_hashes.json,
+    made by tests/golden/make_feature_off_hashes.py with that library)."""
     from golden.make_feature_off_hashes import fingerprint
     ref = json.load(open(os.path.join(HERE, "golden", "feature_off_hashes.json")))
     for c in ref["cases"]:

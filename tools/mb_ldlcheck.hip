@@ -70,9 +70,10 @@ int main() {
     for (int j = 0; j < N; ++j) {
       for (int i = 0; i < N; ++i) {
         double f = F[i * N + j];
-        if (i > j) { double e = fabs(f - L[i * N + j] * Dg[j]); if (e > ecol) { ecol = e; bi = i; bj = j; } }
-        if (i < j) erow = fmax(erow, fabs(f - L[j * N + i] * Dg[i]));
-        if (i == j) ediag = fmax(ediag, fabs(f - Dg[j]));
+        // ldl_rows' output: row k of every column pre-scaled by -1/D_k (the diagonal -> -1)
+        if (i > j) { double e = fabs(f + L[i * N + j] * Dg[j] / Dg[i]); if (e > ecol) { ecol = e; bi = i; bj = j; } }
+        if (i < j) erow = fmax(erow, fabs(f + L[j * N + i]));
+        if (i == j) ediag = fmax(ediag, fabs(f + 1.0));
       }
       edinv = fmax(edinv, fabs(F[4 * N * N + j] * Dg[j] - 1.0));
     }

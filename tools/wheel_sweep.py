@@ -58,5 +58,8 @@ for tol, eps in settings:
                           "status": np.bincount(st, minlength=4).tolist(),
                           "iters_mean": float(it.mean()), "iters_max": int(it.max()),
                           "err_max": float(err.max()), "err_med": float(np.median(err)),
+                          "err_max_ok": float(err[st[:nor] == 0].max()) if (st[:nor] == 0).any() else None,
+                          "not_ok_sample": [(int(e), int(st[e]), float(err[e]))
+                                            for e in np.nonzero(st[:nor] != 0)[0]],
                           "not_ok": np.nonzero(st != 0)[0][:20].tolist()}), flush=True)
     s.close()
