@@ -134,9 +134,14 @@ int osc_model_destroy(osc_model* model);
 int osc_model_get_desc(const osc_model* model, osc_model_desc* desc);
 
 /* Device scratch the solve needs for `nenv` environments: the per-env reduced QP handed from
- * the assembly kernel to the interior-point kernel (8.5 KB Go2 / 12.3 KB WaLTER per env), then
- * 4 B per env of solve-status scratch used by the warm-start fix-up pass. */
+ * the assembly kernel to the interior-point kernel (osc_workspace_env_bytes per env, env-major
+ * from the start of the buffer), then solver scratch the interior point writes: 4 B per env of
+ * solve-status scratch for the warm-start fix-up pass, and the lockstep compaction's park area
+ * (the interior-point state of envs parked mid-solve, 1.4 KB Go2 / 1.9 KB WaLTER per env), slot
+ * list and counter. */
 int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
+/* Bytes of one environment's reduced-QP block at the start of the workspace (its stride). */
+int osc_workspace_env_bytes(const osc_model* model, size_t* bytes);
 
 /* Batched solve; see the header comment for layouts.  Device pointers, async on `stream`.
  * `workspace` (16-byte aligned, >= osc_workspace_bytes) may be NULL: the library then takes
@@ -154,7 +159,7 @@ int osc_batch_solve(const osc_model* model, int32_t nenv,
  * and writes the outputs exactly as osc_batch_solve does (contact_mask must be the one assembled
  * with).  Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its layout per
  * environment, in doubles: [g (NY, padded even) | U (NU x (NY+1) padded) | Hr (NY x NY) |
- * X (NX x (NY+1) padded)]; stride osc_workspace_bytes / nenv.  Two coordinate systems
+ * X (NX x (NY+1) padded)]; stride osc_workspace_env_bytes.  Two coordinate systems
  * (DESIGN.md §3): y = (dv_a, z) with dv_b = X [y;1], NX = nv - nu, u = U [y;1] (walter_sr), or
  * y = (u, z) with dv = X [y;1], NX = nv and no U block (u = y_u; unitree_go2). */
 int osc_batch_assemble(const osc_model* model, int32_t nenv,

@@ -206,6 +206,25 @@ constexpr bool hr_fits_lds() {   // four one-wave workgroups per CU, 160 KB of L
   return IpmLayout<D, true>::IL * 8 * kEnvPerWave * 4 <= 160 * 1024;
 }
 
+// ---- Lockstep compaction (batches past one resident wavefront per SIMD).
+// The four envs of a wavefront iterate in lockstep, so a wave costs its slowest env's iteration
+// count.  The park pass (CP = 1) stops every wave at the top of iteration park_it: an env not
+// converged by then is PARKED -- its interior-point state (y, s, lambda, carried rp) written to
+// a slot of the park area, its env index to the slot list -- and the wave finishes the rest
+// (refinement, outputs) without it.  The resume pass (CP = 2) packs the parked envs four to a
+// wavefront (slot order) and continues them from iteration park_it.  Every row of a wave
+// evolves independently (only wave-uniform gates couple them), so each env takes exactly the
+// steps it takes in one pass: results are bitwise those of the single pass.
+struct ParkArgs {
+  int32_t* list;    // [nenv]  env of each parked slot
+  int32_t* count;   // parked envs (zeroed before the park pass)
+  double* park;     // [nenv][park_doubles<D>()]  y (32) | s | lambda | rp (NRL x 16 each)
+  int park_it;      // iteration at whose top the park pass parks
+};
+constexpr int kCpNone = 0, kCpPark = 1, kCpResume = 2;
+template <class D>
+constexpr int park_doubles() { return 2 * kRow + 3 * D::NRL * kRow; }
+
 // Upper-triangle pair tables (i <= j), built at compile time.
 template <int N, bool SKIP_CORNER>
 struct Pairs {
@@ -1405,12 +1424,14 @@ constexpr int ipm_lds_doubles() {
 // doubles of LDS.  Wrapped by osc_ipm_kernel (one model) and osc_ipm_pair_kernel (two models).
 // WARM = false compiles none of the warm-start / fix-up logic (the cold solve's register budget
 // is unchanged by it: the two-wave Go2 variant would otherwise spill more).
-template <class D, bool SMALL, bool WARM, int RF_ = kRfNone>
+template <class D, bool SMALL, bool WARM, int RF_ = kRfNone, int CP = kCpNone>
 __device__ __forceinline__ void ipm_block(
     const DevParams* __restrict__ P, int blk, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm,
-    int flags, double* __restrict__ sm) {
+    int flags, double* __restrict__ sm, ParkArgs PA = ParkArgs{}) {
+  static_assert(CP == kCpNone || (!WARM && RF_ == kRfFused && !D::WH),
+                "compaction: cold solves with the fused refinement only");
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NY = D::NY, NY1P = D::NY1P, MI = D::MI,
                 NRL = D::NRL;
   // flags: bit 0 = the cold fix-up pass after a warm-started solve, bit 1 = hand the multipliers
@@ -1423,9 +1444,14 @@ __device__ __forceinline__ void ipm_block(
   using LY = IpmLayout<D, HRL>;
   const int lane = threadIdx.x;
   const int grp = lane / kRow, l = lane % kRow;
+  // resume pass: the wave's rows are parked slots (env_raw), their envs from the slot list
+  const int cnt = CP == kCpResume ? *PA.count : nenv;
+  if (CP == kCpResume && blk * kEnvPerWave >= cnt) return;
   const int env_raw = blk * kEnvPerWave + grp;
-  const bool valid = env_raw < nenv;
-  const int env = valid ? env_raw : nenv - 1;   // spare rows replay the last env, write nothing
+  const bool valid = env_raw < cnt;
+  const int env = CP == kCpResume ? PA.list[valid ? env_raw : cnt - 1]
+                                  : (valid ? env_raw : nenv - 1);   // spare rows replay the last
+                                                                     // env, write nothing
   // Fix-up pass after a warm-started solve: only wavefronts holding an env that did not converge
   // run (cold, from the same workspace); only those envs' outputs are rewritten.
   bool write_out = valid;
@@ -1457,10 +1483,14 @@ __device__ __forceinline__ void ipm_block(
   // Hr columns are addressed as wave-uniform base (SGPR pair) + 32-bit lane offset + immediate:
   // 64-bit per-lane address registers for 48 loads do not fit, and their spill reloads
   // (scratch loads share vmcnt) used to serialise the whole prefetch.
+  // (resume pass: the rows' envs are anywhere in the batch -- the base is the workspace itself
+  // and the lane offset the env's whole one; launch_t keeps nenv x WS below 2^32 doubles)
   const double* __restrict__ wsw =
-      ws + static_cast<size_t>(blk) * kEnvPerWave * D::WS + D::W_HR;   // L2-resident
-  const unsigned lane_off = static_cast<unsigned>(env - blk * kEnvPerWave) *
-                            static_cast<unsigned>(D::WS);
+      ws + (CP == kCpResume ? size_t{0} : static_cast<size_t>(blk) * kEnvPerWave * D::WS) +
+      D::W_HR;   // L2-resident
+  const unsigned lane_off =
+      static_cast<unsigned>(CP == kCpResume ? env : env - blk * kEnvPerWave) *
+      static_cast<unsigned>(D::WS);
   double* sG = B + LY::I_G;
   double* sVy = B + LY::I_VY;
   double* sVy2 = B + LY::I_VY2;
@@ -1831,6 +1861,30 @@ __device__ __forceinline__ void ipm_block(
     any_warm = __ballot(warm) != 0;
     all_warm = __ballot(!warm) == 0;
   }
+  // Compaction (ParkArgs): the park slot's state, exactly as the park pass left it at the top of
+  // iteration park_it (the y slots of every lane, v1 or not; s, lambda, rp of every row slot).
+  const int pslot = env_raw < cnt ? env_raw : cnt - 1;
+  auto park_at = [&](int slot) {
+    return PA.park + static_cast<size_t>(slot) * park_doubles<D>();
+  };
+  auto resume_state = [&]() -> int {
+    if constexpr (CP == kCpResume) {
+      const double* pk = park_at(pslot);
+      y0 = pk[l];
+      y1 = pk[kRow + l];
+#pragma unroll
+      for (int t = 0; t < NRL; ++t) {
+        s[t] = pk[2 * kRow + l + kRow * t];
+        lam[t] = pk[2 * kRow + NRL * kRow + l + kRow * t];
+        rp[t] = pk[2 * kRow + 2 * NRL * kRow + l + kRow * t];
+      }
+      sVy[j0] = y0;
+      if (v1) sVy[j1] = y1;
+      wave_sync();
+    }
+    return PA.park_it;
+  };
+  bool parked = false;   // park pass: this row's env went to the park area (no outputs here)
   if constexpr (REFINE) {
     // the interior point's result for this env (osc_ipm_kernel, W_SOL): y, and the active rows
     // as lambda > s with lambda = q > 0
@@ -1855,7 +1909,7 @@ __device__ __forceinline__ void ipm_block(
     if (v1) sVy[j1] = y1;
     wave_sync();
   } else
-  for (int it = all_warm ? 0 : -1;; ++it) {
+  for (int it = CP == kCpResume ? resume_state() : (all_warm ? 0 : -1);; ++it) {
     STAMP_BEGIN();
     const bool init = it < 0;
     double mu = 0.0;
@@ -1939,6 +1993,29 @@ __device__ __forceinline__ void ipm_block(
         done = true;
         st = OSC_SOLVE_OK;
         it_done = it;
+      }
+      if constexpr (CP == kCpPark) {
+        if (it == PA.park_it && __ballot(!done) != 0) {
+          // one slot per unconverged row (lane 0 of the row takes it), its state written by
+          // every lane of the row; the row then counts as done in this wave
+          int slot = 0;
+          if (!done && l == 0) slot = atomicAdd(PA.count, 1);
+          slot = __shfl(slot, grp * kRow, kWave);
+          if (!done) {
+            double* pk = park_at(slot);
+            pk[l] = y0;
+            pk[kRow + l] = y1;
+#pragma unroll
+            for (int t = 0; t < NRL; ++t) {
+              pk[2 * kRow + l + kRow * t] = s[t];
+              pk[2 * kRow + NRL * kRow + l + kRow * t] = lam[t];
+              pk[2 * kRow + 2 * NRL * kRow + l + kRow * t] = rp[t];
+            }
+            if (l == 0) PA.list[slot] = env;
+            parked = true;
+            done = true;
+          }
+        }
       }
       if (__ballot(!done) == 0 || it >= P->max_iter) {
         if (!done) it_done = it;
@@ -2178,6 +2255,7 @@ __device__ __forceinline__ void ipm_block(
   // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
   // discarded.
   bool refined = false;
+  if constexpr (CP == kCpPark) write_out = write_out && !parked;   // the resume pass writes them
   // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
   // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
   // every other multiplier from the design vector itself.
@@ -2225,6 +2303,8 @@ __device__ __forceinline__ void ipm_block(
       const double* rG = kRefG ? wenv + D::W_GD : sRG;
       constexpr int kUr = kRefG ? 2 : 32;   // workspace reads: few in flight (registers)
       double dlast = 0.0;   // WH: the last refinement step's size (its convergence test)
+      bool settled = false;                          // this env's final round is done
+      double yk0 = 0.0, yk1 = 0.0, dk = 0.0, nuk = 0.0;   // its result (WH: step, multiplier)
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
       // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
@@ -2302,7 +2382,8 @@ __device__ __forceinline__ void ipm_block(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             static_for<0, kEnvPerWave>([&](auto G) {
               constexpr int g = decltype(G)::value;
-              const int eg = blk * kEnvPerWave + g < nenv ? blk * kEnvPerWave + g : nenv - 1;
+              const int eg = CP == kCpResume ? __builtin_amdgcn_readlane(env, g * kRow)
+                             : (blk * kEnvPerWave + g < nenv ? blk * kEnvPerWave + g : nenv - 1);
               const double2* src =
                   reinterpret_cast<const double2*>(ws + static_cast<size_t>(eg) * D::WS + D::W_X);
               static_for<0, NT>([&](auto T) {
@@ -2508,8 +2589,26 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         viol_env = mine && row_max(nviol) > 0.0;
+        // an env whose round ended without a violation is final: a further round that a wave-mate
+        // asks for must not move it (its multipliers carry over between rounds), so each env's
+        // result is independent of the envs sharing its wavefront -- and of the compaction's
+        // packing (ParkArgs)
+        if (mine && !viol_env && !settled) {
+          settled = true;
+          yk0 = ya0;
+          yk1 = ya1;
+          if constexpr (WHR) {
+            dk = dlast;
+            nuk = l < NW ? sWNu[l] : 0.0;
+          }
+        }
         STAMP_END(11);
         if (__ballot(viol_env) == 0) break;
+      }
+      if (settled) {
+        ya0 = yk0;
+        ya1 = yk1;
+        if constexpr (WHR) dlast = dk;
       }
       // keep the refined iterate when it is feasible, finite and close to the interior point's
       const double mv = fmax(fabs(ya0 - y0), v1 ? fabs(ya1 - y1) : 0.0);
@@ -2546,7 +2645,7 @@ __device__ __forceinline__ void ipm_block(
              64 * (wres <= ytol ? 0 : 1) + 128 * (row_min(dlast <= 1e-10 * (1.0 + myr) ? 1.0 : 0.0) == 1.0 ? 0 : 1) +
              256 * (row_min(mv <= 0.1 * (1.0 + myr) ? 1.0 : 0.0) == 1.0 ? 0 : 1);
 #endif
-      put_wheel_duals((mine && keep && l < NW) ? sWNu[l] : 0.0);
+      put_wheel_duals((mine && keep && l < NW) ? (settled ? nuk : sWNu[l]) : 0.0);
       wave_sync();
       sVy[j0] = y0;
       if (v1) sVy[j1] = y1;
@@ -2637,6 +2736,18 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_kernel(
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, RF>()];
   ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                     gstatus, giters, gwarm, flags, sm);
+}
+
+// The cold fused solve split in two passes for lockstep compaction (ParkArgs): CP = kCpPark
+// over every env's wavefront, then CP = kCpResume over the parked envs, packed.
+template <class D, bool SMALL, int CP>
+__global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_ipm_compact_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
+    int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, int flags, ParkArgs PA) {
+  __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, kRfFused>()];
+  ipm_block<D, SMALL, false, kRfFused, CP>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau,
+                                           gx, gstatus, giters, nullptr, flags, sm, PA);
 }
 
 // The full-space refinement pass (torque coordinates): the same body with the interior-point
@@ -2924,6 +3035,36 @@ int ws_doubles(KernelId k) {
   }
 }
 
+// Park iteration per model (0: compaction off).  Measured (tools/park_sweep.py,
+// profiles/r03_park_sweep.txt): WaLTER (one wavefront per SIMD at every batch size) gains from
+// it; Go2's two-wave kernel loses -- its parked envs run their last iterations as a serial tail
+// after the park pass instead of hidden behind other wavefronts.
+int park_iter_default(KernelId k) { return k == K_WALTER ? 16 : 0; }
+
+int park_doubles_of(KernelId k) {
+  switch (k) {
+    case K_GO2: return park_doubles<Go2>();
+    case K_WALTER: return park_doubles<Walter>();
+    default: return 0;   // (no compaction with wheel rows)
+  }
+}
+
+// Byte offsets of the workspace blocks (all 16-byte aligned).
+struct WsLayout {
+  size_t status, park, list, count, total;
+};
+WsLayout ws_layout(KernelId k, int32_t nenv) {
+  const size_t n = static_cast<size_t>(nenv);
+  auto pad = [](size_t b) { return (b + 15) & ~static_cast<size_t>(15); };
+  WsLayout w;
+  w.status = sizeof(double) * static_cast<size_t>(ws_doubles(k)) * n;
+  w.park = w.status + pad(sizeof(int32_t) * n);
+  w.list = w.park + sizeof(double) * static_cast<size_t>(park_doubles_of(k)) * n;
+  w.count = w.list + pad(sizeof(int32_t) * n);
+  w.total = w.count + (park_doubles_of(k) ? 16 : 0);
+  return w;
+}
+
 int dual_rows(KernelId k) {
   switch (k) {
     case K_GO2: return Go2::NV + 4 * Go2::NC + Go2::NX;
@@ -2942,6 +3083,8 @@ struct osc_model {
   int device;
   int small_batch_max;   // envs that fit one wavefront per SIMD (4 per wave x 4 SIMDs x CUs)
   bool refine;           // torque-coordinate model with refinement steps > 0
+  int resident_envs;     // envs of one wavefront per SIMD over the whole device
+  int park_it;           // compaction's park iteration (0: off; ParkArgs)
 };
 
 extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
@@ -3044,6 +3187,12 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   m->small_batch_max = (kid == K_GO2) ? kEnvPerWave * 4 * cus : INT32_MAX;
   if (const char* e = std::getenv("OSC_SMALL_BATCH_MAX")) m->small_batch_max = std::atoi(e);
   if (kid == K_WALTER_WHEELS) m->small_batch_max = INT32_MAX;   // (one-wave kernel only)
+  // Lockstep compaction past one resident wavefront per SIMD (ParkArgs); the
+  // variable exists for the A/B sweeps (0 switches it off)
+  m->resident_envs = kEnvPerWave * 4 * cus;
+  m->park_it = park_iter_default(kid);
+  if (const char* e = std::getenv("OSC_PARK_IT")) m->park_it = std::atoi(e);
+  if (kid == K_WALTER_WHEELS || m->park_it < 0 || m->park_it >= hp.restart_iter) m->park_it = 0;
   if (hipMalloc(&m->dparams, sizeof(DevParams)) != hipSuccess ||
       hipMemcpy(m->dparams, &hp, sizeof(DevParams), hipMemcpyHostToDevice) != hipSuccess) {
     if (m->dparams) (void)hipFree(m->dparams);
@@ -3076,10 +3225,15 @@ extern "C" int osc_model_get_desc(const osc_model* model, osc_model_desc* desc) 
 
 extern "C" int osc_workspace_bytes(const osc_model* model, int32_t nenv, size_t* bytes) {
   if (!model || !bytes || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
-  // per-env reduced QPs, then int32 solve-status scratch for the warm fix-up pass (16-B padded)
-  const size_t n = static_cast<size_t>(nenv);
-  *bytes = sizeof(double) * static_cast<size_t>(ws_doubles(model->kid)) * n +
-           ((sizeof(int32_t) * n + 15) & ~static_cast<size_t>(15));
+  // per-env reduced QPs, then int32 solve-status scratch for the warm fix-up pass (16-B padded),
+  // then the compaction's park area, slot list and counter (ParkArgs)
+  *bytes = ws_layout(model->kid, nenv).total;
+  return OSC_OK;
+}
+
+extern "C" int osc_workspace_env_bytes(const osc_model* model, size_t* bytes) {
+  if (!model || !bytes) return OSC_ERR_INVALID_ARGUMENT;
+  *bytes = sizeof(double) * static_cast<size_t>(ws_doubles(model->kid));
   return OSC_OK;
 }
 
@@ -3119,7 +3273,31 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     // 65,536 warm 50.0 -> 44.5 M solves/s), so that case keeps the separate refinement pass.
     const bool fused = warm == nullptr && model->refine;
     const bool fused_warm = small && warm != nullptr && model->refine;
-    if (warm == nullptr) {
+    // Lockstep compaction: more wavefronts than SIMDs, so the SIMD time the lockstep tail costs
+    // is time other wavefronts could use (ParkArgs; bitwise the single pass's results)
+    const bool compact = fused && !D::WH && model->park_it > 0 && nenv > model->resident_envs &&
+                         static_cast<size_t>(nenv) * D::WS < (size_t{1} << 32);
+    if (warm == nullptr && compact) {
+      const WsLayout wl = ws_layout(model->kid, nenv);
+      char* base = reinterpret_cast<char*>(ws);
+      ParkArgs pa;
+      pa.park = reinterpret_cast<double*>(base + wl.park);
+      pa.list = reinterpret_cast<int32_t*>(base + wl.list);
+      pa.count = reinterpret_cast<int32_t*>(base + wl.count);
+      pa.park_it = model->park_it;
+      (void)hipMemsetAsync(pa.count, 0, sizeof(int32_t), s);
+      if (small) {
+        hipLaunchKernelGGL((osc_ipm_compact_kernel<D, true, kCpPark>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
+        hipLaunchKernelGGL((osc_ipm_compact_kernel<D, true, kCpResume>), dim3(nb), dim3(kWave), 0,
+                           s, model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
+      } else {
+        hipLaunchKernelGGL((osc_ipm_compact_kernel<D, false, kCpPark>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
+        hipLaunchKernelGGL((osc_ipm_compact_kernel<D, false, kCpResume>), dim3(nb), dim3(kWave), 0,
+                           s, model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
+      }
+    } else if (warm == nullptr) {
       if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);

@@ -21,6 +21,7 @@ SOLVE_OK, SOLVE_MAX_ITER, SOLVE_NUMERICAL, SOLVE_UNREFINED = 0, 1, 2, 3
 
 EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_from_yaml",
                     "osc_model_destroy", "osc_model_get_desc", "osc_workspace_bytes",
+                    "osc_workspace_env_bytes",
                     "osc_batch_solve", "osc_batch_assemble", "osc_batch_solve_assembled",
                     "osc_status_string", "osc_abi_version",
                     "osc_pd_base_targets", "osc_contact_mask_from_contacts",
@@ -131,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.osc_model_get_desc.restype = ctypes.c_int
     L.osc_workspace_bytes.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t)]
     L.osc_workspace_bytes.restype = ctypes.c_int
+    L.osc_workspace_env_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t)]
+    L.osc_workspace_env_bytes.restype = ctypes.c_int
     L.osc_batch_solve.argtypes = [vp, i32] + [vp] * 10 + [vp, ctypes.c_size_t, vp]
     L.osc_batch_solve.restype = ctypes.c_int
     L.osc_status_string.argtypes = [ctypes.c_int]

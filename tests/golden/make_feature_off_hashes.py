@@ -7,8 +7,10 @@ mask, nenv, seed) batch.  tests/test_gpu_wheels.py checks that the current build
 them, i.e. that models without wheel no-slip rows -- the feature-off path -- are bitwise what
 they were.  History: made with the round-2 build; regenerated once in round 3 for the
 intentional change of the LDL factor's storage (row k pre-scaled by -1/D_k, multiply-free
-triangular solves: DESIGN.md §5); the wheel rows' changes since do not reach models without
-them.  Regenerate
+triangular solves: DESIGN.md §5), and again for the refinement rounds settling per env (an env
+whose round ends without a violation keeps that round's result when a wave-mate asks for another
+round: results no longer depend on which envs share a wavefront); the wheel rows' changes do not
+reach models without them.  Regenerate
 only for an intentional numerical change of the default kernels, and say so in the commit.
 """
 from __future__ import annotations

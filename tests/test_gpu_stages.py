@@ -36,9 +36,11 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     inp = generate(robot, nenv, SEED_BASE + 31, "tumbling", mask_mode)
     args = s.prepare(**inp)
     L = _lib.lib()
-    nbytes = ctypes.c_size_t()
+    nbytes, ebytes = ctypes.c_size_t(), ctypes.c_size_t()
     assert L.osc_workspace_bytes(s._h, nenv, ctypes.byref(nbytes)) == 0
-    sz = nbytes.value // 8 // nenv
+    assert L.osc_workspace_env_bytes(s._h, ctypes.byref(ebytes)) == 0
+    sz = ebytes.value // 8
+    assert nbytes.value >= sz * 8 * nenv
     ev = lambda a: (a + 1) // 2 * 2
     ny1p = ev(ny + 1)
     # layout documented in include/osc_batch.h: torque coordinates (both robots by default,
@@ -53,13 +55,13 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     o_gd = o_hd + nv * nv
     nrl = (2 * nu + 6 * nc + 15) // 16
     assert sz == o_gd + ev(nv) + ev(ny) + nrl * 16 + 2
-    dbg = torch.zeros((nenv, sz), dtype=torch.float64, device=gpu)
+    dbg = torch.zeros((nbytes.value // 8,), dtype=torch.float64, device=gpu)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     rc = L.osc_batch_assemble(s._h, nenv, *[p(a) for a in args], p(dbg), nbytes,
                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     assert rc == 0
     torch.cuda.synchronize()
-    D = dbg.cpu().numpy()
+    D = dbg.cpu().numpy()[:nenv * sz].reshape(nenv, sz)
     model = load_model(robot)
     rng = np.random.default_rng(0)
     for e in range(nenv):
@@ -132,3 +134,51 @@ def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
         outs.append(o)
     for k in ("tau", "x", "status", "iters"):
         assert torch.equal(getattr(outs[0], k), getattr(outs[1], k)), k
+
+
+@pytest.mark.parametrize("robot,nenv,scenario,park", [
+    ("walter_sr", 20480, "tumbling", None),     # the default park iteration (compaction on)
+    ("unitree_go2", 20480, "tumbling", "11"),   # forced: the two-wave kernel's park / resume
+])
+def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park, monkeypatch):
+    """Lockstep compaction (ParkArgs): envs not converged at the park iteration
+    continue in a second pass, packed four to a wavefront -- each env takes exactly the steps it
+    takes in one pass, so tau, x, status and iters are bitwise those of the single pass."""
+    from osc_amd.solver import OSCBatchSolver
+    inp = generate(robot, nenv, SEED_BASE + 34, scenario, "bernoulli")
+    outs = []
+    for p in (park, "0"):
+        if p is None:
+            monkeypatch.delenv("OSC_PARK_IT", raising=False)
+        else:
+            monkeypatch.setenv("OSC_PARK_IT", p)
+        s = OSCBatchSolver(robot)
+        args = s.prepare(**inp)
+        o = s.alloc_outputs(nenv, want_x=True)
+        s.solve_into(o, *args)
+        torch.cuda.synchronize()
+        outs.append(o)
+    it = outs[1].iters.cpu().numpy()
+    assert (it > int(park or 16)).any() and (it <= int(park or 16)).any()   # both passes ran
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(outs[0], k), getattr(outs[1], k)), k
+
+
+@pytest.mark.parametrize("robot,nenv,seed", [("walter_sr", 4096, 23), ("unitree_go2", 8192, 22)])
+def test_results_independent_of_wave_mates(gpu, robot, nenv, seed):
+    """Every env's result is bitwise independent of the envs that share its wavefront: the
+    permuted batch returns the permuted results.  (The refinement repeats a round for the whole
+    wavefront when one env's refined point violates a row; an env whose round ended without a
+    violation keeps that round's result -- before round 3 it was refined again, at rounding
+    level, whenever a wave-mate asked.  The seeds are the feature-off fingerprint batches, which
+    hold such wavefronts.)"""
+    from osc_amd.solver import OSCBatchSolver
+    s = OSCBatchSolver(robot)
+    inp = generate(robot, nenv, SEED_BASE + seed, "tumbling", "bernoulli")
+    perm = np.random.default_rng(5).permutation(nenv)
+    a = s.solve(**inp, want_x=True)
+    b = s.solve(**{k: v[perm] for k, v in inp.items()}, want_x=True)
+    torch.cuda.synchronize()
+    pt = torch.from_numpy(perm).to(a.tau.device)
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(a, k)[pt], getattr(b, k)), k
