@@ -1,13 +1,13 @@
 # Round-3: settle-per-env refinement rounds: size of the change against the previous head's
-# library (tools/dump_tau.py), feature-off fingerprints regenerated, the GPU suite, default bench.
+# library (tools/dump_cases.py), feature-off fingerprints regenerated, the GPU suite, default bench.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 export TMPDIR=/tmp
 O=gpurun_out/r03zc
 mkdir -p $O
-OSC_LIB_PATH=operational-space-control_amd/lib/ablate/r03head/libosc_batch.so timeout -k 10 200 python tools/dump_tau.py $O/tau_head.npz > $O/dump_head.log 2>&1 || exit 10
-timeout -k 10 200 python tools/dump_tau.py $O/tau_new.npz > $O/dump_new.log 2>&1 || exit 11
+OSC_LIB_PATH=operational-space-control_amd/lib/ablate/r03head/libosc_batch.so timeout -k 10 200 python tools/dump_cases.py $O/tau_head.npz > $O/dump_head.log 2>&1 || exit 10
+timeout -k 10 200 python tools/dump_cases.py $O/tau_new.npz > $O/dump_new.log 2>&1 || exit 11
 timeout -k 10 120 python tests/golden/make_feature_off_hashes.py > $O/feature_off_hashes.json 2> $O/hashes.err || exit 12
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --deselect tests/test_gpu_wheels.py::test_feature_off_bitwise_unchanged > $O/gpu_tests.log 2>&1 || exit 13
 timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 14
