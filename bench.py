@@ -572,6 +572,7 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
             traffic = tj.get("per_kernel", {}).get("osc_ipm_kernel")
     flops = algorithmic_flops(args.robot, mean_iters)
     tflops = flops * nenv / (kernel_ms * 1e-3) / 1e12
+    ipm_name = ipm_kernel_name(args.robot, nenv, dev)
     line = {
         "metric": METRIC,
         "value": value,
@@ -592,20 +593,20 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
                    "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
+                     "kernel": ipm_name, "kernel_ms": ipm_ms,
                      "kernel_ms_from": f"HIP events around the kernel on every "
                                        f"{max(1, args.event_every)}-th timed step (the "
                                        f"full-space refinement runs inside it)",
                      "bytes_per_solve": bps,
                      "inputs": "cache-warm: the same batch every step (its 31 MB stays in the "
                                "256 MB Infinity Cache); the kernel is latency-bound",
-                     "solve_pair": {"kernel": "osc_setup_kernel + osc_ipm_kernel",
+                     "solve_pair": {"kernel": f"osc_setup_kernel + {ipm_name}",
                                     "kernel_ms": kernel_ms, "achieved": achieved_pair,
                                     "frac": achieved_pair / HBM_PEAK_GBS,
                                     "traffic": traffic_pair,
                                     "kernel_ms_split": {"osc_setup_kernel": setup_ms,
-                                                        "osc_ipm_kernel": ipm_ms}}},
-        "roofline_fp64": {"kernel": "osc_setup_kernel + osc_ipm_kernel", "achieved": tflops,
+                                                        ipm_name: ipm_ms}}},
+        "roofline_fp64": {"kernel": f"osc_setup_kernel + {ipm_name}", "achieved": tflops,
                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / FP64_PEAK_TFLOPS,
                           "flops_per_solve": flops, "mean_ipm_iters": mean_iters},
@@ -649,6 +650,17 @@ def single_env(robot: str, ticks: int) -> dict:
                    "(MJCF tree) + reduced QP + interior point (warm), D2H; wall time per tick")
     res["reference_period_us"] = 2000
     return res
+
+
+def ipm_kernel_name(robot: str, nenv: int, dev) -> str:
+    """The interior-point kernel(s) one launch runs: past one resident wavefront per SIMD the
+    cold WaLTER solve of at least four rounds of wavefronts runs the lockstep compaction's park and resume passes (csrc/osc_batch.hip,
+    ParkArgs; the default park iteration is 16 for WaLTER, off for Go2; OSC_PARK_IT overrides)."""
+    resident = 4 * 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+    park = os.environ.get("OSC_PARK_IT", "16" if robot == "walter_sr" else "0")
+    if nenv >= 4 * resident and park not in ("", "0"):   # (kParkMinRounds)
+        return "osc_ipm_compact_kernel (park + resume passes)"
+    return "osc_ipm_kernel"
 
 
 def main(argv=None) -> None:

@@ -3040,6 +3040,7 @@ int ws_doubles(KernelId k) {
 // it; Go2's two-wave kernel loses -- its parked envs run their last iterations as a serial tail
 // after the park pass instead of hidden behind other wavefronts.
 int park_iter_default(KernelId k) { return k == K_WALTER ? 16 : 0; }
+constexpr int kParkMinRounds = 4;   // batches of at least this many resident-wave rounds
 
 int park_doubles_of(KernelId k) {
   switch (k) {
@@ -3275,7 +3276,11 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     const bool fused_warm = small && warm != nullptr && model->refine;
     // Lockstep compaction: more wavefronts than SIMDs, so the SIMD time the lockstep tail costs
     // is time other wavefronts could use (ParkArgs; bitwise the single pass's results)
-    const bool compact = fused && !D::WH && model->park_it > 0 && nenv > model->resident_envs &&
+    // (from four rounds of wavefronts per SIMD: at two, WaLTER configs[3] -- 8,192 tumbling envs,
+    // masks redrawn -- is 4 % slower with it, 17.0 vs 17.7 M solves/s; at eight, 32,768, 3 %
+    // faster: profiles/r03ze_*)
+    const bool compact = fused && !D::WH && model->park_it > 0 &&
+                         nenv >= kParkMinRounds * model->resident_envs &&
                          static_cast<size_t>(nenv) * D::WS < (size_t{1} << 32);
     if (warm == nullptr && compact) {
       const WsLayout wl = ws_layout(model->kid, nenv);

@@ -137,7 +137,7 @@ def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
 
 
 @pytest.mark.parametrize("robot,nenv,scenario,park", [
-    ("walter_sr", 20480, "tumbling", None),     # the default park iteration (compaction on)
+    ("walter_sr", 20480, "tumbling", None),     # the default park iteration (compaction on: 5 rounds)
     ("unitree_go2", 20480, "tumbling", "11"),   # forced: the two-wave kernel's park / resume
 ])
 def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park, monkeypatch):
