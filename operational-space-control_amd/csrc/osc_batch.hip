@@ -2279,7 +2279,11 @@ __device__ __forceinline__ void ipm_block(
   // the duals ask the refinement for more steps (its multipliers converge more slowly than y)
   const int refine_steps = P->refine_steps + ((D::WH && want_dual) ? P->refine_dual_extra : 0);
   if constexpr (RF != kRfNone) {
-    const bool mine = valid && st == OSC_SOLVE_OK;
+    // WH: an env the interior point left at max_iter is refined too (its rotated Newton systems
+    // can stall short of eps_mu with the active set already right): a kept refinement -- no row
+    // violated, no multiplier of the wrong sign, its last step converged -- is a KKT point of the
+    // strictly convex QP, i.e. its optimum, and the env reports OK
+    const bool mine = valid && (st == OSC_SOLVE_OK || (WHR && st == OSC_SOLVE_MAX_ITER));
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
       const double ytol = 1e-9 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)));
@@ -2304,6 +2308,7 @@ __device__ __forceinline__ void ipm_block(
       constexpr int kUr = kRefG ? 2 : 32;   // workspace reads: few in flight (registers)
       double dlast = 0.0;   // WH: the last refinement step's size (its convergence test)
       bool settled = false;                          // this env's final round is done
+      const double yscale = WHR ? row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)) : 0.0;
       double yk0 = 0.0, yk1 = 0.0, dk = 0.0, nuk = 0.0;   // its result (WH: step, multiplier)
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
@@ -2589,11 +2594,14 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         viol_env = mine && row_max(nviol) > 0.0;
+        // WH: a round whose steps have not converged asks for another one as well (it restarts
+        // from the interior point's iterate with the multipliers carried over)
+        const bool more = viol_env || (WHR && mine && dlast > 1e-10 * (1.0 + yscale));
         // an env whose round ended without a violation is final: a further round that a wave-mate
         // asks for must not move it (its multipliers carry over between rounds), so each env's
         // result is independent of the envs sharing its wavefront -- and of the compaction's
         // packing (ParkArgs)
-        if (mine && !viol_env && !settled) {
+        if (mine && !more && !settled) {
           settled = true;
           yk0 = ya0;
           yk1 = ya1;
@@ -2603,11 +2611,12 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         STAMP_END(11);
-        if (__ballot(viol_env) == 0) break;
+        if (__ballot(more && !settled) == 0) break;
       }
-      if (settled) {
+      if (settled) {   // (its own last round had no violation, whatever later rounds found)
         ya0 = yk0;
         ya1 = yk1;
+        viol_env = false;
         if constexpr (WHR) dlast = dk;
       }
       // keep the refined iterate when it is feasible, finite and close to the interior point's
@@ -2635,10 +2644,11 @@ __device__ __forceinline__ void ipm_block(
         y0 = ya0;
         y1 = ya1;
         refined = true;
+        st = OSC_SOLVE_OK;
       }
       // a converged env whose refinement is rejected keeps the interior point's iterate, and says
       // so: it is only as accurate as the interior point's stop
-      if (mine && !keep) st = OSC_SOLVE_UNREFINED;
+      if (mine && !keep && st == OSC_SOLVE_OK) st = OSC_SOLVE_UNREFINED;
 #ifdef OSC_REFINE_DIAG   // diagnostic builds only: why the refinement was rejected
       if (mine && !keep)
         st = OSC_SOLVE_UNREFINED + 16 * (viol_env ? 1 : 0) + 32 * (row_min(ok) == 1.0 ? 0 : 1) +

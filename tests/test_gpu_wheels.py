@@ -37,7 +37,7 @@ NORM_ACH, ELEM_ACH = 1e-9, 1e-7
 # (Gram-Schmidt in dv and y space) land within 1.7e-8 of the oracle on the worst of
 # 1,024 numpy-restated envs, median 1e-13 -- hence also a median bar.
 WHEEL_NORM, WHEEL_ELEM, WHEEL_MEDIAN = 1e-8, 1e-6, 1e-10
-WHEEL_OK_FRAC = {"standing": 1.0, "tumbling": 0.9}
+WHEEL_OK_FRAC = {"standing": 1.0, "tumbling": 0.95}
 # KKT certificate of the GPU's (x, y), each residual scaled as oracle/qp_exact.kkt_certificate.
 # Stationarity: the duals are recovered from x (osc_dual_kernel), so it measures x's optimality
 # through H_dv and M^-1 -- a design vector 1e-9 off in dv shows up as ~1e-8..1e-7 here (WaLTER).
@@ -94,8 +94,8 @@ def test_wheel_rows_vs_oracle(gpu, scenario, mask_mode, seed):
     torch.cuda.synchronize()
     st = res.status.cpu().numpy()
     # every env converges standing; tumbling (masked wheels, degenerate active sets) a few are
-    # reported as not converged / not refined (DESIGN.md §3 measures ~3.6 % of 2,048) -- flagged,
-    # never returned as OK: the OK ones are held to the oracle
+    # reported as not converged / not refined (DESIGN.md §3.1 measures 0.5-0.7 % of 2,048) --
+    # flagged, never returned as OK: the OK ones are held to the oracle
     ok_frac = WHEEL_OK_FRAC[scenario]
     assert (st == 0).mean() >= ok_frac, np.bincount(st)
     x = res.x.cpu().numpy()
@@ -287,7 +287,7 @@ def test_wheel_rows_kkt_certificate(gpu):
     s.solve_into(out, *args, wheel_dir=wdt)
     torch.cuda.synchronize()
     st = out.status.cpu().numpy()
-    assert (st == 0).mean() >= 0.95, (np.bincount(st), np.nonzero(st)[0][:20])
+    assert (st == 0).mean() >= 0.98, (np.bincount(st), np.nonzero(st)[0][:20])
     cert = _kkt(*_batched_qp("walter_sr_wheels", *args, wheel, wdt), out.x, out.y)
     ok = torch.from_numpy(st == 0).cuda()
     # known gap: the rows' multipliers come from the refinement's last residual, and
