@@ -139,6 +139,8 @@ def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
 @pytest.mark.parametrize("robot,nenv,scenario,park", [
     ("walter_sr", 20480, "tumbling", None),     # the default park iteration (compaction on: 5 rounds)
     ("unitree_go2", 20480, "tumbling", "11"),   # forced: the two-wave kernel's park / resume
+    ("walter_sr", 16387, "standing", None),     # ragged: a partial last wavefront, parked slots
+    ("unitree_go2", 16390, "standing", "12"),   # not a multiple of four
 ])
 def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park, monkeypatch):
     """Lockstep compaction (ParkArgs): envs not converged at the park iteration
