@@ -3147,8 +3147,12 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.max_iter = d.max_iter;
   // warm start: numpy-model studies on a 1 % random walk; the OSC_WARM_* variables
   // exist for the diagnostic sweeps (tools/warm_stalls.py), not for production use
-  hp.warm_delta = 0.1;
-  hp.warm_center = 0.3;
+  // (round 3, bench.py warm object, profiles/r03_warm_settings.txt: delta 0.1 -> 1 and centring
+  // 0.3 -> 1 cut the slowest warm envs' tail -- Go2 4,096 24.1 -> 27.2 M, WaLTER 4,096 14.0 ->
+  // 20.0 M, WaLTER tumbling 8,192 20.0 -> 22.5 M solves/s -- for +0.8 / +1.1 mean iterations:
+  // Go2 65,536 52.4 -> 51.6 M)
+  hp.warm_delta = 1.0;
+  hp.warm_center = 1.0;
   hp.warm_restart = 22;
   hp.restart_iter = 28;
   // full-space refinement: two steps with one factorisation, penalty 1e2 x the
