@@ -1456,7 +1456,11 @@ __device__ __forceinline__ void ipm_block(
   // run (cold, from the same workspace); only those envs' outputs are rewritten.
   bool write_out = valid;
   if constexpr (WARM) {
-    const bool redo = valid && fixup && gstatus[env] != OSC_SOLVE_OK;
+    // (not an env the warm pass converged whose refinement was rejected, OSC_SOLVE_UNREFINED: a
+    // cold solve rejects the same refinement -- measured on the joint-state control loop, where
+    // redoing them cost a cold wavefront per tick, tools/warm_qpos_status.py)
+    const bool redo = valid && fixup && gstatus[env] != OSC_SOLVE_OK &&
+                      gstatus[env] != OSC_SOLVE_UNREFINED;
     if (fixup && __ballot(redo) == 0) return;
     write_out = valid && (!fixup || redo);
   }
