@@ -3,7 +3,7 @@ counts, and for envs whose full-space refinement was rejected, why (OSC_REFINE_D
 3 + 16 rows still violated after the last round + 32 move too large / not finite) and how far
 the returned torques are from the exact oracle.
 
-    OSC_LIB_PATH=<diag lib> python tools/qpos_refine_diag.py [nenv]
+    OSC_LIB_PATH=<diag lib> python tools/qpos_refine_diag.py [nenv] [env,env,...]
 """
 import json
 import os
@@ -39,6 +39,8 @@ vals, cnt = np.unique(st, return_counts=True)
 print(json.dumps({"status_codes": dict(zip(map(int, vals), map(int, cnt)))}), flush=True)
 model = load_model(robot)
 bad = np.nonzero(st != 0)[0][:12]
+if len(sys.argv) > 2:   # also these envs, whatever their status (e.g. an earlier build's rejects)
+    bad = np.union1d(bad, np.array([int(v) for v in sys.argv[2].split(",")]))
 M, C, J, b = (t.cpu().numpy() for t in (kout.M, kout.C, kout.J, kout.b))
 Tn, mk = d["T"], d["mask"]
 tau = res.tau.cpu().numpy()
