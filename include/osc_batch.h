@@ -78,7 +78,8 @@ typedef enum {
   OSC_SOLVE_UNREFINED = 3         /* converged (complementarity <= eps_mu) but the full-space
                                      refinement was rejected: the interior point's iterate is
                                      returned, accurate only to its stop (~1e-5 normwise at
-                                     eps_mu 1e-9)                               */
+                                     eps_mu 1e-9 on the synthetic batches; up to
+                                     ~1e-2 on ill-conditioned joint-state QPs) */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C
@@ -179,8 +180,9 @@ int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double
  * it has no inequality rows.  Each call reads the state and writes this tick's solution back.
  * Results agree with the cold solve to the solve's tolerance; the iteration count drops when
  * consecutive ticks are close.  A warm env that stalls is re-centred in place,
- * and any env the warm pass leaves unconverged is re-solved cold by a second launch that only
- * the wavefronts holding such an env execute. */
+ * and any env the warm pass leaves unconverged (OSC_SOLVE_MAX_ITER / _NUMERICAL) is re-solved
+ * cold by a second launch that only the wavefronts holding such an env execute (an
+ * OSC_SOLVE_UNREFINED env is not: the cold solve rejects the same refinement). */
 int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
 int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
                          const double* M, const double* C, const double* J, const double* b,
