@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define OSC_ABI_VERSION 2
+#define OSC_ABI_VERSION 3
 #define OSC_MAX_SITES 32
 #define OSC_MAX_NU 16
 
@@ -76,10 +76,12 @@ typedef enum {
   OSC_SOLVE_MAX_ITER = 1,         /* iteration cap reached; best iterate returned             */
   OSC_SOLVE_NUMERICAL = 2,        /* non-finite values encountered (e.g. NaN inputs)         */
   OSC_SOLVE_UNREFINED = 3         /* converged (complementarity <= eps_mu) but the full-space
-                                     refinement was rejected: the interior point's iterate is
-                                     returned, accurate only to its stop (~1e-5 normwise at
-                                     eps_mu 1e-9 on the synthetic batches; up to
-                                     ~1e-2 on ill-conditioned joint-state QPs) */
+                                     refinement found no KKT point within its rounds (or was
+                                     forced off by osc_model_tuning.refine_max_move): the
+                                     interior point's iterate is returned, accurate only to its
+                                     stop (up to ~2e-2 normwise at eps_mu 1e-9
+                                     along the internal-force directions).  Measured: none on
+                                     the synthetic and joint-state test batches since round 4   */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C
@@ -126,6 +128,40 @@ int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_model_desc*
  * the current HIP device. */
 int osc_model_create(const osc_model_desc* desc, osc_model** out);
 
+/* Solver policy knobs (ABI 3).  A release library reads no environment variable: what used to be
+ * OSC_* variables is this explicit block, filled with the model's defaults by
+ * osc_model_tuning_defaults and passed to osc_model_create_tuned.  None of them changes the QP;
+ * they change how the interior point and the refinement get to its optimum (and so the last
+ * bits of the result), or which kernel variant runs.  For experiments and tests. */
+typedef struct {
+  int32_t refine_steps;           /* full-space refinement: minimum steps per round (each env
+                                     stops at its own convergence, at most 8); 0 = no
+                                     refinement, the interior point then runs to eps_mu <= 1e-12.
+                                     Default 2 (wheel rows: 8, fixed)                            */
+  double refine_max_move;         /* reject a refinement that moves y by more than this x
+                                     (1 + |y|) (OSC_SOLVE_UNREFINED).  Default 1e300 (none: a
+                                     kept refinement is a KKT point, i.e. the optimum)           */
+  double eps_mu;                  /* interior-point stop; default the descriptor's eps_mu        */
+  int32_t restart_iter;           /* cold: an env still far off (mu > 1e-6) is re-centred at this
+                                     iteration.  Default 28                                      */
+  int32_t warm_restart;           /* warm-started: the same.  Default 22                         */
+  double warm_delta;              /* warm start: slacks / multipliers floored here.  Default 1   */
+  double warm_center;             /* warm start: no pair below this x their mean.  Default 1     */
+  double wheel_tol;               /* wheel rows: residual needed to stop.  Default 1e-6          */
+  int32_t small_batch_max;        /* the one-wave interior-point kernel up to this batch, the
+                                     two-wave one above; -1 = the device's resident batch (4 envs
+                                     per wave x 4 SIMDs x CUs) for Go2, always one-wave WaLTER   */
+  int32_t park_it;                /* lockstep compaction's park iteration; 0 = off; -1 = model
+                                     default (WaLTER 16, Go2 off)                                */
+} osc_model_tuning;
+
+/* Fill `tuning` with the defaults of the model `desc` describes (host-only). */
+int osc_model_tuning_defaults(const osc_model_desc* desc, osc_model_tuning* tuning);
+
+/* osc_model_create with explicit tuning (NULL = the defaults). */
+int osc_model_create_tuned(const osc_model_desc* desc, const osc_model_tuning* tuning,
+                           osc_model** out);
+
 /* Convenience: osc_desc_from_yaml + osc_model_create. */
 int osc_model_create_from_yaml(const char* robot, const char* yaml_path, osc_model** out);
 
@@ -156,20 +192,25 @@ int osc_batch_solve(const osc_model* model, int32_t nenv,
 /* The two halves of osc_batch_solve, for callers that time, overlap or reuse them.
  * osc_batch_assemble builds every environment's reduced QP (the six CasADi evaluations +
  * OSQP stacking of operational_space_controller.h:457-529, condensed onto NY = nu + 3nc reduced
- * variables y) into `workspace`; osc_batch_solve_assembled runs the interior-point solve on it
- * and writes the outputs exactly as osc_batch_solve does (contact_mask must be the one assembled
- * with).  Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its layout per
- * environment, in doubles: [g (NY, padded even) | U (NU x (NY+1) padded) | Hr (NY x NY) |
- * X (NX x (NY+1) padded)]; stride osc_workspace_env_bytes.  Two coordinate systems
- * (DESIGN.md §3): y = (dv_a, z) with dv_b = X [y;1], NX = nv - nu, u = U [y;1] (walter_sr), or
- * y = (u, z) with dv = X [y;1], NX = nv and no U block (u = y_u; unitree_go2). */
+ * variables y = (u, z)) into `workspace`; osc_batch_solve_assembled runs the interior-point solve
+ * on it and writes the outputs exactly as osc_batch_solve does (contact_mask must be the one
+ * assembled with).  Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its
+ * layout per environment, in doubles: [g (NY, padded even) | Hr (NY x NY, padded
+ * even) | X (nv x (NY+1), row stride padded even) | H_dv (nv x nv) | f_dv (nv, padded even) |
+ * solver hand-off], stride osc_workspace_env_bytes, with dv = X [y; 1] = M^-1 (B u + Jc z - C),
+ * H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t) (wheel rows: further blocks).
+ * The solve WRITES to the workspace: its per-env hand-off blocks and, past the reduced QPs, the
+ * solve-status scratch, the lockstep compaction's park area, slot list and counter
+ * -- one workspace serves one solve at a time; concurrent solves on several streams need a
+ * workspace each (the reduced-QP blocks themselves are only read, so the same assembled QPs may
+ * be copied and solved again). */
 int osc_batch_assemble(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask,
                        void* workspace, size_t workspace_bytes, void* stream);
 int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double* contact_mask,
                               double* tau, double* x, int32_t* status, int32_t* iters,
-                              const void* workspace, size_t workspace_bytes, void* stream);
+                              void* workspace, size_t workspace_bytes, void* stream);
 
 /* Warm start across control ticks -- the reference's OsqpSolver::SetWarmStart with the previous
  * tick's primal/dual solution (operational_space_controller.h:519-526).  `warm_state` is a
@@ -194,7 +235,7 @@ int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
                                    const double* contact_mask, double* tau, double* x,
                                    int32_t* status, int32_t* iters,
                                    double* warm_state, size_t warm_state_bytes,
-                                   const void* workspace, size_t workspace_bytes, void* stream);
+                                   void* workspace, size_t workspace_bytes, void* stream);
 
 /* One model's batch inside a multi-model call: the arguments of osc_batch_solve for that model
  * (device pointers; `workspace` required, >= osc_workspace_bytes(model, nenv), 16-B aligned). */

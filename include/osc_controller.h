@@ -125,6 +125,10 @@ class OperationalSpaceController {
   int last_solve_status();
   int last_iterations();
   const osc_model_desc& desc() const { return desc_; }
+  /* Replay the tick as one captured hipGraph instead of direct launches (default off: measured
+   * slower on ROCm 7, Go2 tick median 98 vs 92 us; profiles/r02_tick_graph_ab.txt).  Call before
+   * initialize_thread. */
+  void set_tick_graph(bool on) { use_graph_ = on; }
 
  private:
   Status tick_locked();
@@ -175,8 +179,7 @@ class OperationalSpaceController {
   void* graph_exec_ = nullptr;      // hipGraphExec_t of the captured tick
   int graph_kind_ = -1;
   size_t graph_in_bytes_ = 0;
-  bool use_graph_ = false;          // OSC_TICK_GRAPH=1: replay the tick as a hipGraph (measured
-                                    // slower on ROCm 7: Go2 tick median 98 vs 92 us direct)
+  bool use_graph_ = false;          // set_tick_graph: replay the tick as a hipGraph
 };
 
 }  // namespace osc_amd

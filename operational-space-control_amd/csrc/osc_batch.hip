@@ -1381,6 +1381,9 @@ struct RefineLds {
 // (osc_refine_kernel), or both in one wavefront (every cold solve and the one-wave warm solve:
 // no hand-off, no second launch).
 constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
+// Full-space refinement without wheel rows: rounds of active-set changes, and
+// steps per round at most (each env stops at its own convergence, at least refine_steps)
+constexpr int kRefineRounds = 4, kRefineMaxSteps = 8;
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
@@ -2310,14 +2313,20 @@ __device__ __forceinline__ void ipm_block(
       const double* rH = kRefG ? wenv + D::W_HD : sRH;
       const double* rG = kRefG ? wenv + D::W_GD : sRG;
       constexpr int kUr = kRefG ? 2 : 32;   // workspace reads: few in flight (registers)
-      double dlast = 0.0;   // WH: the last refinement step's size (its convergence test)
+      double dlast = 0.0;   // the last refinement step's size (its convergence test)
       bool settled = false;                          // this env's final round is done
-      const double yscale = WHR ? row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)) : 0.0;
+      const double yscale = row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0));
       double yk0 = 0.0, yk1 = 0.0, dk = 0.0, nuk = 0.0;   // its result (WH: step, multiplier)
+      // (no wheel rows) steps run until the env's own step has converged -- at least
+      // refine_steps, at most kRefineMaxSteps per round -- and then the env is frozen (its later
+      // lockstep steps are zero), so its result does not depend on its wave-mates' step counts
+      bool conv = false;
       // rounds: a row the refined point violates was active at the optimum with a vanishing
       // multiplier (lambda and s both ~1e-6 when the interior point stops): it joins the active
-      // set and the round repeats from the interior point's iterate (numpy model: <= 2 rounds)
-      for (int round = 0; round < (WHR ? 5 : 3); ++round) {
+      // set, a row whose multiplier came out negative leaves it, and the round repeats from the
+      // interior point's iterate with the multipliers carried over (numpy model of the kernel on
+      // joint-state batches, tools/kkt_study.py: <= 3 rounds, <= 9 steps)
+      for (int round = 0; round < (WHR ? 5 : kRefineRounds); ++round) {
         STAMP_BEGIN();
 #ifdef OSC_STAMPS
         st_acc[10] += 1ull << 40;   // rounds, in the top bits of the assembly+LDL slot
@@ -2439,7 +2448,8 @@ __device__ __forceinline__ void ipm_block(
         wave_sync();
         STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
-        for (int k = 0; k < refine_steps; ++k) {
+        conv = false;
+        for (int k = 0; k < (WHR ? refine_steps : kRefineMaxSteps); ++k) {
           // WH: X holds X^ = X'T, so dv = X^ [y^; 1] (y^ = T'y staged in sVy2, free until the step)
           // and the rows' residual at y comes with y^
           const double* yv = sVy;
@@ -2563,17 +2573,30 @@ __device__ __forceinline__ void ipm_block(
             rot_out(d0, d1, d0, d1);
             dlast = row_max(fmax(fabs(d0), v1 ? fabs(d1) : 0.0));
           }
+          const bool frz = !WHR && conv;   // converged at an earlier step: no further move
+          if (frz) {
+            d0 = 0.0;
+            d1 = 0.0;
+          }
           sVy2[j0] = d0;
           if (v1) sVy2[j1] = d1;
           wave_sync();
 #pragma unroll
-          for (int t = 0; t < NRL; ++t) mur[t] += Dr[t] * (Gv(sVy2, t) + R3[t]);
+          for (int t = 0; t < NRL; ++t) mur[t] += frz ? 0.0 : Dr[t] * (Gv(sVy2, t) + R3[t]);
           ya0 += d0;
           ya1 += d1;
           wave_sync();
           sVy[j0] = ya0;
           if (v1) sVy[j1] = ya1;
           wave_sync();
+          if constexpr (!WHR) {
+            // converged: the step fell below 1e-10 of the env's |y| (a row-wide scale: a lane
+            // holding only near-zero variables must not hold the env to 1e-10 absolute)
+            const double dn = row_max(fmax(fabs(d0), v1 ? fabs(d1) : 0.0));
+            if (!frz) dlast = dn;
+            conv = conv || (k + 1 >= refine_steps && dn <= 1e-10 * (1.0 + yscale));
+            if (k + 1 >= refine_steps && __ballot(mine && !conv) == 0) break;
+          }
         }
         // rows the refined point violates join the active set
         double nviol = 0.0;
@@ -2583,9 +2606,10 @@ __device__ __forceinline__ void ipm_block(
           Dr[t] = v ? dpen : Dr[t];
           nviol += v ? 1.0 : 0.0;
         }
-        if constexpr (WHR) {
-          // ... and (WH, whose slack-based active set can include a row the optimum leaves) rows
-          // whose multiplier came out negative leave it
+        {
+          // ... and rows whose multiplier came out negative leave it (WH: its slack-based active
+          // set can include a row the optimum leaves; otherwise a row the interior point's
+          // lambda > s test took with a vanishing multiplier)
           double mmax = 0.0;
 #pragma unroll
           for (int t = 0; t < NRL; ++t) mmax = fmax(mmax, Dr[t] != 0.0 ? fabs(mur[t]) : 0.0);
@@ -2598,9 +2622,10 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         viol_env = mine && row_max(nviol) > 0.0;
-        // WH: a round whose steps have not converged asks for another one as well (it restarts
+        // a round whose steps have not converged asks for another one as well (it restarts
         // from the interior point's iterate with the multipliers carried over)
-        const bool more = viol_env || (WHR && mine && dlast > 1e-10 * (1.0 + yscale));
+        const bool more =
+            viol_env || (mine && (WHR ? dlast > 1e-10 * (1.0 + yscale) : !conv));
         // an env whose round ended without a violation is final: a further round that a wave-mate
         // asks for must not move it (its multipliers carry over between rounds), so each env's
         // result is independent of the envs sharing its wavefront -- and of the compaction's
@@ -2623,19 +2648,22 @@ __device__ __forceinline__ void ipm_block(
         viol_env = false;
         if constexpr (WHR) dlast = dk;
       }
-      // keep the refined iterate when it is feasible, finite and close to the interior point's
+      // Keep the refined iterate when it is a KKT point of the QP: its last round added no row
+      // (primal feasible to ytol), dropped no row (no multiplier of the wrong sign) and its steps
+      // converged, and it is finite.  The QP is strictly convex, so that point is its optimum,
+      // however far the interior point's iterate was from it: with the internal-force curvature
+      // 2 w_reg = 2e-4, the barrier of a nearly active row pushes the iterate at mu = 1e-9 up to
+      // ~2e-2 off along such directions (joint-state batches, tools/kkt_study.py) -- the move
+      // bound 1e-3 per lane that stood here rejected those envs (OSC_SOLVE_UNREFINED).
+      // refine_max_move (default: none) remains as a tuning knob that forces rejections.
       const double mv = fmax(fabs(ya0 - y0), v1 ? fabs(ya1 - y1) : 0.0);
-      const double my = fmax(fabs(y0), v1 ? fabs(y1) : 0.0);
-      // (WH: the interior point stops earlier (eps_mu 1e-9, osc_model_create: past that its
-      // rotated Newton systems lose accuracy), so the refinement may move y further; it is kept
-      // when it has converged -- its last step below 1e-10 of y -- within 0.1 of y)
-      // (WH: both tests against the env's |y| scale, row_max: dlast is a row-wide maximum, and a
-      // lane holding only near-zero variables must not hold it to 1e-10 absolute)
-      const double myr = WHR ? row_max(my) : my;
+      const double myr = row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0));
+      // (WH: the rotated Newton systems; kept when converged -- its last step below 1e-10 of the
+      // env's |y| scale, a row-wide maximum -- within 0.1 of y)
       const double ok =
           (isfinite(ya0) && isfinite(ya1) &&
            (WHR ? (mv <= 0.1 * (1.0 + myr) && dlast <= 1e-10 * (1.0 + myr))
-                : mv <= P->refine_max_move * (1.0 + my))) ? 1.0 : 0.0;
+                : (settled && mv <= P->refine_max_move * (1.0 + myr)))) ? 1.0 : 0.0;
       // (WH: and the wheel rows hold at the refined point)
       double wres = 0.0;
       if constexpr (WHR) {
@@ -3102,7 +3130,62 @@ struct osc_model {
   int park_it;           // compaction's park iteration (0: off; ParkArgs)
 };
 
+namespace {
+// Model defaults of the knobs in osc_model_tuning.
+void tuning_defaults(const osc_model_desc& d, osc_model_tuning& t) {
+  std::memset(&t, 0, sizeof(t));
+  // full-space refinement: at least two steps per round with one factorisation,
+  // each env until its own step converges (numpy model: <= 3e-12 normwise on Go2 / WaLTER
+  // batches, from up to 2e-2 without it); wheel rows: eight, run to convergence from the interior
+  // point's earlier stop
+  t.refine_steps = d.wheel_rows ? 8 : 2;
+  t.refine_max_move = 1e300;
+  t.eps_mu = d.eps_mu;
+  // warm start (round 3, profiles/r03_warm_settings.txt: delta 0.1 -> 1 and
+  // centring 0.3 -> 1 cut the slowest warm envs' tail -- Go2 4,096 24.1 -> 27.2 M, WaLTER 4,096
+  // 14.0 -> 20.0 M, WaLTER tumbling 8,192 20.0 -> 22.5 M solves/s -- for +0.8 / +1.1 mean
+  // iterations: Go2 65,536 52.4 -> 51.6 M)
+  t.warm_delta = 1.0;
+  t.warm_center = 1.0;
+  t.warm_restart = 22;
+  t.restart_iter = 28;
+  // wheel no-slip rows: pinned coordinates of the interior point's Newton
+  // systems, so every step leaves them holding to rounding; the stop test asks 1e-6
+  t.wheel_tol = 1e-6;
+  t.small_batch_max = -1;
+  t.park_it = -1;
+}
+
+#ifdef OSC_TUNING_ENV
+// Diagnostic builds only (tools/*.sh sweeps): the OSC_* variables override the tuning block.  A
+// release library reads no environment variable.
+void tuning_from_env(osc_model_tuning& t) {
+  if (const char* e = std::getenv("OSC_REFINE_STEPS")) t.refine_steps = std::atoi(e);
+  if (const char* e = std::getenv("OSC_EPS_MU")) t.eps_mu = std::atof(e);
+  if (const char* e = std::getenv("OSC_RESTART_ITER")) t.restart_iter = std::atoi(e);
+  if (const char* e = std::getenv("OSC_WARM_RESTART")) t.warm_restart = std::atoi(e);
+  if (const char* e = std::getenv("OSC_WARM_DELTA")) t.warm_delta = std::atof(e);
+  if (const char* e = std::getenv("OSC_WARM_CENTER")) t.warm_center = std::atof(e);
+  if (const char* e = std::getenv("OSC_REFINE_MAX_MOVE")) t.refine_max_move = std::atof(e);
+  if (const char* e = std::getenv("OSC_WHEEL_TOL")) t.wheel_tol = std::atof(e);
+  if (const char* e = std::getenv("OSC_SMALL_BATCH_MAX")) t.small_batch_max = std::atoi(e);
+  if (const char* e = std::getenv("OSC_PARK_IT")) t.park_it = std::atoi(e);
+}
+#endif
+}  // namespace
+
+extern "C" int osc_model_tuning_defaults(const osc_model_desc* desc, osc_model_tuning* tuning) {
+  if (!desc || !tuning) return OSC_ERR_INVALID_ARGUMENT;
+  tuning_defaults(*desc, *tuning);
+  return OSC_OK;
+}
+
 extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
+  return osc_model_create_tuned(desc, nullptr, out);
+}
+
+extern "C" int osc_model_create_tuned(const osc_model_desc* desc, const osc_model_tuning* tuning,
+                                      osc_model** out) {
   if (!desc || !out) return OSC_ERR_INVALID_ARGUMENT;
   *out = nullptr;
   const osc_model_desc& d = *desc;
@@ -3146,48 +3229,39 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   hp.mu = d.mu;
   hp.w_torque = d.w_torque;
   hp.w_reg = d.w_reg;
-  hp.eps_mu = d.eps_mu;
+  osc_model_tuning t;
+  if (tuning) {
+    t = *tuning;
+  } else {
+    tuning_defaults(d, t);
+#ifdef OSC_TUNING_ENV
+    tuning_from_env(t);
+#endif
+  }
+  if (t.refine_steps < 0 || t.restart_iter < 0 || t.warm_restart < 0 || !(t.eps_mu > 0.0) ||
+      !(t.refine_max_move >= 0.0) || !(t.wheel_tol > 0.0) || !(t.warm_delta > 0.0) ||
+      !(t.warm_center >= 0.0) || t.park_it < -1 || t.small_batch_max < -1)
+    return OSC_ERR_INVALID_ARGUMENT;
+  hp.eps_mu = t.eps_mu;
   hp.inf_thresh = thresh;
   hp.max_iter = d.max_iter;
-  // warm start: numpy-model studies on a 1 % random walk; the OSC_WARM_* variables
-  // exist for the diagnostic sweeps (tools/warm_stalls.py), not for production use
-  // (round 3, bench.py warm object, profiles/r03_warm_settings.txt: delta 0.1 -> 1 and centring
-  // 0.3 -> 1 cut the slowest warm envs' tail -- Go2 4,096 24.1 -> 27.2 M, WaLTER 4,096 14.0 ->
-  // 20.0 M, WaLTER tumbling 8,192 20.0 -> 22.5 M solves/s -- for +0.8 / +1.1 mean iterations:
-  // Go2 65,536 52.4 -> 51.6 M)
-  hp.warm_delta = 1.0;
-  hp.warm_center = 1.0;
-  hp.warm_restart = 22;
-  hp.restart_iter = 28;
-  // full-space refinement: two steps with one factorisation, penalty 1e2 x the
-  // largest reduced-Hessian diagonal (numpy model: <= 3e-12 normwise on Go2 / WaLTER batches,
-  // from up to 7e-6 without it)
-  // (wheel rows: eight, run to convergence from the interior point's earlier stop)
-  hp.refine_steps = d.wheel_rows ? 8 : 2;
-  hp.refine_penalty = 1e2;
-  if (const char* e = std::getenv("OSC_REFINE_STEPS")) hp.refine_steps = std::atoi(e);
-  if (const char* e = std::getenv("OSC_EPS_MU")) hp.eps_mu = std::atof(e);   // sweeps only
-  if (const char* e = std::getenv("OSC_RESTART_ITER")) hp.restart_iter = std::atoi(e);
-  if (const char* e = std::getenv("OSC_WARM_RESTART")) hp.warm_restart = std::atoi(e);
-  if (const char* e = std::getenv("OSC_WARM_DELTA")) hp.warm_delta = std::atof(e);
-  if (const char* e = std::getenv("OSC_WARM_CENTER")) hp.warm_center = std::atof(e);
-  // a refinement that moves y by more than this (relative) is rejected (OSC_SOLVE_UNREFINED);
-  // the variable exists so a test can force rejections
-  hp.refine_max_move = 1e-3;
+  hp.warm_delta = t.warm_delta;
+  hp.warm_center = t.warm_center;
+  hp.warm_restart = t.warm_restart;
+  hp.restart_iter = t.restart_iter;
+  hp.refine_steps = t.refine_steps;
+  hp.refine_penalty = 1e2;   // active-row penalty of the refinement, x max diag(Hr)
+  hp.refine_max_move = t.refine_max_move;
   hp.refine_dual_extra = 4;
-  if (const char* e = std::getenv("OSC_REFINE_MAX_MOVE")) hp.refine_max_move = std::atof(e);
   // The YAML's Go2 stop (eps_mu 1e-9) presumes the refinement finishes the solve; without it the
   // interior point runs to 1e-12 itself.
   if (hp.refine_steps <= 0) hp.eps_mu = std::fmin(hp.eps_mu, 1e-12);
-  // wheel no-slip rows: pinned coordinates of the interior point's Newton systems,
-  // so every step leaves them holding to rounding; the stop test asks 1e-6
   for (int i = 0; i < OSC_MAX_SITES; ++i) hp.wheel_dof[i] = -1;
   for (int i = 0; d.wheel_rows && i < d.nc; ++i) {
     hp.wheel_dof[i] = d.wheel_dof[i];
     hp.wheel_radius[i] = d.wheel_radius[i];
   }
-  hp.wheel_tol = 1e-6;
-  if (const char* e = std::getenv("OSC_WHEEL_TOL")) hp.wheel_tol = std::atof(e);
+  hp.wheel_tol = t.wheel_tol;
 
   osc_model* m = new (std::nothrow) osc_model;
   if (!m) return OSC_ERR_DEVICE;
@@ -3204,14 +3278,12 @@ extern "C" int osc_model_create(const osc_model_desc* desc, osc_model** out) {
   // two waves' register budget (scratch spills): it always runs one wave per SIMD with AGPR
   // spill space (MI355X, 32,768 envs: 2.61 vs 2.95 ms; tools/variant_sweep.sh).
   m->small_batch_max = (kid == K_GO2) ? kEnvPerWave * 4 * cus : INT32_MAX;
-  if (const char* e = std::getenv("OSC_SMALL_BATCH_MAX")) m->small_batch_max = std::atoi(e);
+  if (t.small_batch_max >= 0) m->small_batch_max = t.small_batch_max;
   if (kid == K_WALTER_WHEELS) m->small_batch_max = INT32_MAX;   // (one-wave kernel only)
-  // Lockstep compaction past one resident wavefront per SIMD (ParkArgs); the
-  // variable exists for the A/B sweeps (0 switches it off)
+  // Lockstep compaction past one resident wavefront per SIMD (ParkArgs; 0 = off)
   m->resident_envs = kEnvPerWave * 4 * cus;
-  m->park_it = park_iter_default(kid);
-  if (const char* e = std::getenv("OSC_PARK_IT")) m->park_it = std::atoi(e);
-  if (kid == K_WALTER_WHEELS || m->park_it < 0 || m->park_it >= hp.restart_iter) m->park_it = 0;
+  m->park_it = t.park_it >= 0 ? t.park_it : park_iter_default(kid);
+  if (kid == K_WALTER_WHEELS || m->park_it >= hp.restart_iter) m->park_it = 0;
   if (hipMalloc(&m->dparams, sizeof(DevParams)) != hipSuccess ||
       hipMemcpy(m->dparams, &hp, sizeof(DevParams), hipMemcpyHostToDevice) != hipSuccess) {
     if (m->dparams) (void)hipFree(m->dparams);
@@ -3560,20 +3632,20 @@ extern "C" int osc_batch_solve_warm(const osc_model* model, int32_t nenv, const 
 extern "C" int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,
                                               const double* contact_mask, double* tau, double* x,
                                               int32_t* status, int32_t* iters, double* warm_state,
-                                              size_t warm_state_bytes, const void* workspace,
+                                              size_t warm_state_bytes, void* workspace,
                                               size_t workspace_bytes, void* stream) {
   if (!warm_small(model, nenv, warm_state, warm_state_bytes)) return OSC_ERR_INVALID_ARGUMENT;
   return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, nullptr, contact_mask, tau, x,
-                status, iters, const_cast<void*>(workspace), workspace_bytes, stream,
+                status, iters, workspace, workspace_bytes, stream,
                 kInteriorPoint, warm_state);
 }
 
 extern "C" int osc_batch_solve_assembled(const osc_model* model, int32_t nenv,
                                          const double* contact_mask, double* tau, double* x,
-                                         int32_t* status, int32_t* iters, const void* workspace,
+                                         int32_t* status, int32_t* iters, void* workspace,
                                          size_t workspace_bytes, void* stream) {
   return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, nullptr, contact_mask, tau, x,
-                status, iters, const_cast<void*>(workspace), workspace_bytes, stream,
+                status, iters, workspace, workspace_bytes, stream,
                 kInteriorPoint);
 }
 

@@ -150,7 +150,6 @@ Status OperationalSpaceController::initialize_optimization() {
     return InternalError("pinned host allocation failed");
   }
   std::memset(h_in_, 0, in_doubles * sizeof(double));
-  if (const char* e = std::getenv("OSC_TICK_GRAPH")) use_graph_ = std::atoi(e) != 0;
   optimization_initialized_ = true;
   return Status::Ok();
 }
@@ -285,7 +284,7 @@ Status OperationalSpaceController::enqueue_tick_locked(int kind, size_t in_bytes
   return Status::Ok();
 }
 
-// The tick as one hipGraph (OSC_TICK_GRAPH=1): captured on the first tick of a kind and replayed
+// The tick as one hipGraph (set_tick_graph(true)): captured on the first tick of a kind and replayed
 // afterwards (one submission instead of two copies, three or four kernel launches and two
 // copies).  A capture the runtime refuses falls back to launching the same work directly.  Off by
 // default: on MI355X / ROCm 7 the replay is slower than the direct launches from pinned staging

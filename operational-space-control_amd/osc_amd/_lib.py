@@ -34,7 +34,8 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_kin_desc_from_mjcf", "osc_kin_desc_from_mjcf_robot",
                     "osc_contact_geom_table", "osc_tumbling_params_default",
                     "osc_tumbling_targets", "osc_dual_rows", "osc_batch_solve_ex",
-                    "osc_batch_assemble_ex")
+                    "osc_batch_assemble_ex", "osc_model_tuning_defaults",
+                    "osc_model_create_tuned")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -58,6 +59,17 @@ class OscModelDesc(ctypes.Structure):
         ("wheel_rows", ctypes.c_int32),
         ("wheel_dof", ctypes.c_int32 * OSC_MAX_SITES),
         ("wheel_radius", ctypes.c_double * OSC_MAX_SITES),
+    ]
+
+
+class OscModelTuning(ctypes.Structure):
+    """osc_model_tuning (include/osc_batch.h, ABI 3): solver policy knobs, no QP change."""
+    _fields_ = [
+        ("refine_steps", ctypes.c_int32), ("refine_max_move", ctypes.c_double),
+        ("eps_mu", ctypes.c_double), ("restart_iter", ctypes.c_int32),
+        ("warm_restart", ctypes.c_int32), ("warm_delta", ctypes.c_double),
+        ("warm_center", ctypes.c_double), ("wheel_tol", ctypes.c_double),
+        ("small_batch_max", ctypes.c_int32), ("park_it", ctypes.c_int32),
     ]
 
 
@@ -124,6 +136,10 @@ def lib() -> ctypes.CDLL:
     L.osc_desc_from_yaml.restype = ctypes.c_int
     L.osc_model_create.argtypes = [dp, ctypes.POINTER(vp)]
     L.osc_model_create.restype = ctypes.c_int
+    L.osc_model_tuning_defaults.argtypes = [dp, ctypes.POINTER(OscModelTuning)]
+    L.osc_model_tuning_defaults.restype = ctypes.c_int
+    L.osc_model_create_tuned.argtypes = [dp, ctypes.POINTER(OscModelTuning), ctypes.POINTER(vp)]
+    L.osc_model_create_tuned.restype = ctypes.c_int
     L.osc_model_create_from_yaml.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(vp)]
     L.osc_model_create_from_yaml.restype = ctypes.c_int
     L.osc_model_destroy.argtypes = [vp]

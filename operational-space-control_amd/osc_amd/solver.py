@@ -39,7 +39,10 @@ class SolveResult:
 
 class OSCBatchSolver:
     def __init__(self, robot: str, yaml_path: str | None = None, eps_mu: float | None = None,
-                 max_iter: int | None = None, device: torch.device | int | None = None):
+                 max_iter: int | None = None, device: torch.device | int | None = None,
+                 tuning: dict | None = None):
+        """tuning: fields of osc_model_tuning (include/osc_batch.h) to change from the model's
+        defaults, e.g. {"small_batch_max": 0} (solver policy only, never the QP)."""
         if not torch.cuda.is_available():
             raise RuntimeError("OSCBatchSolver needs a HIP device (no CPU fallback exists)")
         self.robot = robot
@@ -53,9 +56,19 @@ class OSCBatchSolver:
             desc.max_iter = int(max_iter)
         self.desc = desc
         self.wheels = desc.wheel_rows != 0
+        tune = _lib.OscModelTuning()
+        rc = _lib.lib().osc_model_tuning_defaults(ctypes.byref(desc), ctypes.byref(tune))
+        if rc != 0:
+            raise _lib.OSCError("osc_model_tuning_defaults", rc)
+        for k, v in (tuning or {}).items():
+            if k not in dict(_lib.OscModelTuning._fields_):
+                raise KeyError(f"osc_model_tuning has no field {k!r}")
+            setattr(tune, k, v)
+        self.tuning = tune
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            rc = _lib.lib().osc_model_create(ctypes.byref(desc), ctypes.byref(h))
+            rc = _lib.lib().osc_model_create_tuned(ctypes.byref(desc), ctypes.byref(tune),
+                                                   ctypes.byref(h))
         if rc != 0:
             raise _lib.OSCError("osc_model_create", rc)
         self._h = h

@@ -24,6 +24,8 @@
 #include "osc_controller.h"
 
 using osc_amd::OSCData;
+
+static bool g_tick_graph = false;   // set_tick_graph (main's optional 4th argument)
 using osc_amd::OperationalSpaceController;
 using osc_amd::State;
 using osc_amd::Status;
@@ -90,6 +92,7 @@ static int solve(const std::string& robot, const std::string& path) {
     return Status::Ok();
   };
   OperationalSpaceController c(robot, "", kin, 2000);
+  c.set_tick_graph(g_tick_graph);
   State st = make_state(d.nu, d.nc, 1.0);
   st.contact_mask = f[5];
   Status r = c.initialize(st);
@@ -148,6 +151,7 @@ static int qpos_solve(const std::string& robot, const std::string& path) {
   st.motor_velocity.assign(f[1].begin() + 6, f[1].end());
   st.contact_mask = f[3];
   OperationalSpaceController c(robot);
+  c.set_tick_graph(g_tick_graph);
   Status r = c.initialize(st);
   if (!r.ok()) { std::printf("{\"error\": \"%s\"}\n", r.message().c_str()); return 4; }
   r = c.initialize_optimization();
@@ -192,6 +196,8 @@ static int gpu_lifecycle(const std::string& robot) {
 }
 
 int main(int argc, char** argv) {
+  // solve / qpos <robot> <fixture> [graph]: "1" replays the tick as a captured hipGraph
+  g_tick_graph = argc >= 5 && std::strcmp(argv[4], "1") == 0;
   if (argc >= 4 && std::strcmp(argv[1], "qpos") == 0) return qpos_solve(argv[2], argv[3]);
   if (argc >= 3 && std::strcmp(argv[1], "gpu_lifecycle") == 0) return gpu_lifecycle(argv[2]);
   if (argc >= 3 && std::strcmp(argv[1], "lifecycle") == 0) return lifecycle(argv[2]);

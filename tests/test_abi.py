@@ -24,8 +24,39 @@ def test_library_loads_and_exports_header_symbols():
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.osc_abi_version() == 2
+    assert L.osc_abi_version() == 3
     assert L.osc_status_string(2) == b"OSC_ERR_UNSUPPORTED_DIMS"
+
+
+@pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])
+def test_tuning_defaults(robot):
+    """osc_model_tuning_defaults (ABI 3): the model's solver-policy defaults, host-only."""
+    L = _lib.lib()
+    d = _lib.desc_from_yaml(robot)
+    t = _lib.OscModelTuning()
+    assert L.osc_model_tuning_defaults(ctypes.byref(d), ctypes.byref(t)) == 0
+    assert t.refine_steps == (8 if d.wheel_rows else 2)
+    assert t.refine_max_move == 1e300 and t.eps_mu == d.eps_mu
+    assert (t.restart_iter, t.warm_restart, t.warm_delta, t.warm_center) == (28, 22, 1.0, 1.0)
+    assert t.wheel_tol == 1e-6 and t.small_batch_max == -1 and t.park_it == -1
+    assert L.osc_model_tuning_defaults(None, ctypes.byref(t)) == 1
+    # invalid tuning is refused before any device call
+    h = ctypes.c_void_p()
+    t.refine_steps = -1
+    assert L.osc_model_create_tuned(ctypes.byref(d), ctypes.byref(t), ctypes.byref(h)) in (1, 5)
+
+
+def test_release_library_reads_no_tuning_variables():
+    """The release library reads no OSC_* tuning environment variable: the knobs
+    live in osc_model_tuning; the OSC_TUNING_ENV diagnostic build alone reads them."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for name in (b"OSC_REFINE_STEPS", b"OSC_EPS_MU", b"OSC_RESTART_ITER", b"OSC_WARM_RESTART",
+                 b"OSC_WARM_DELTA", b"OSC_WARM_CENTER", b"OSC_REFINE_MAX_MOVE", b"OSC_WHEEL_TOL",
+                 b"OSC_SMALL_BATCH_MAX", b"OSC_PARK_IT", b"OSC_TICK_GRAPH"):
+        assert name not in blob, name
+    ctrl = os.path.join(os.path.dirname(_lib.LIB_PATH), "libosc_controller.so")
+    if os.path.exists(ctrl):
+        assert b"OSC_TICK_GRAPH" not in open(ctrl, "rb").read()
 
 
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr", "walter_sr_wheels"])

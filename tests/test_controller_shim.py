@@ -36,10 +36,9 @@ def driver():
 
 
 def run(*args, graph=None):
-    env = dict(os.environ)
-    if graph is not None:    # OSC_TICK_GRAPH=1: the tick replayed as one captured hipGraph
-        env["OSC_TICK_GRAPH"] = graph
-    r = subprocess.run([driver(), *args], capture_output=True, text=True, timeout=120, env=env)
+    if graph is not None:    # "1": the tick replayed as one captured hipGraph (set_tick_graph)
+        args = (*args, graph)
+    r = subprocess.run([driver(), *args], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
 

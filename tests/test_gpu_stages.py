@@ -118,15 +118,14 @@ def test_split_stages_equal_fused_solve(gpu):
 
 
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
-def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
+def test_ipm_variants_bitwise_equal(gpu, robot):
     """The one-wave-per-SIMD variant (Hr in LDS where it fits, AGPR spill space) and the
     two-waves variant (Hr streamed from L2) run the same arithmetic: identical outputs."""
     from osc_amd.solver import OSCBatchSolver
     inp = generate(robot, 512, SEED_BASE + 33, "tumbling", "bernoulli")
     outs = []
-    for force in ("100000000", "0"):
-        monkeypatch.setenv("OSC_SMALL_BATCH_MAX", force)
-        s = OSCBatchSolver(robot)
+    for force in (100000000, 0):
+        s = OSCBatchSolver(robot, tuning={"small_batch_max": force})
         args = s.prepare(**inp)
         o = s.alloc_outputs(512, want_x=True)
         s.solve_into(o, *args)
@@ -142,7 +141,7 @@ def test_ipm_variants_bitwise_equal(gpu, robot, monkeypatch):
     ("walter_sr", 16387, "standing", None),     # ragged: a partial last wavefront, parked slots
     ("unitree_go2", 16390, "standing", "12"),   # not a multiple of four
 ])
-def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park, monkeypatch):
+def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park):
     """Lockstep compaction (ParkArgs): envs not converged at the park iteration
     continue in a second pass, packed four to a wavefront -- each env takes exactly the steps it
     takes in one pass, so tau, x, status and iters are bitwise those of the single pass."""
@@ -150,11 +149,7 @@ def test_compaction_bitwise_equal(gpu, robot, nenv, scenario, park, monkeypatch)
     inp = generate(robot, nenv, SEED_BASE + 34, scenario, "bernoulli")
     outs = []
     for p in (park, "0"):
-        if p is None:
-            monkeypatch.delenv("OSC_PARK_IT", raising=False)
-        else:
-            monkeypatch.setenv("OSC_PARK_IT", p)
-        s = OSCBatchSolver(robot)
+        s = OSCBatchSolver(robot, tuning=None if p is None else {"park_it": int(p)})
         args = s.prepare(**inp)
         o = s.alloc_outputs(nenv, want_x=True)
         s.solve_into(o, *args)

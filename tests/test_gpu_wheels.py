@@ -301,14 +301,13 @@ def test_wheel_rows_kkt_certificate(gpu):
     assert frac >= 0.98, (frac, {k: v[ok].max().item() for k, v in cert.items()})
 
 
-def test_rejected_refinement_is_reported(gpu, monkeypatch):
+def test_rejected_refinement_is_reported(gpu):
     """An env whose full-space refinement is rejected keeps the interior point's iterate and is
     reported as OSC_SOLVE_UNREFINED (3), not OK; its torques are only as accurate as the
     interior point's stop (Go2 eps_mu 1e-9: ~1e-5 normwise)."""
     from osc_amd.solver import OSCBatchSolver
-    monkeypatch.setenv("OSC_REFINE_MAX_MOVE", "0")   # every refinement moves y: all rejected
-    s = OSCBatchSolver("unitree_go2")
-    monkeypatch.delenv("OSC_REFINE_MAX_MOVE")
+    # every refinement moves y: all rejected
+    s = OSCBatchSolver("unitree_go2", tuning={"refine_max_move": 0.0})
     d = generate("unitree_go2", 64, SEED_BASE + 88, "tumbling", "bernoulli")
     res = s.solve(**d)
     good = solver("unitree_go2").solve(**d)
