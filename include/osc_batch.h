@@ -137,7 +137,7 @@ typedef struct {
   int32_t refine_steps;           /* full-space refinement: minimum steps per round (each env
                                      stops at its own convergence, at most 8); 0 = no
                                      refinement, the interior point then runs to eps_mu <= 1e-12.
-                                     Default 2 (wheel rows: 8, fixed)                            */
+                                     Default 2 (wheel rows: 12, fixed)                           */
   double refine_max_move;         /* reject a refinement that moves y by more than this x
                                      (1 + |y|) (OSC_SOLVE_UNREFINED).  Default 1e300 (none: a
                                      kept refinement is a KKT point, i.e. the optimum)           */
@@ -274,13 +274,23 @@ typedef struct {
 int osc_dual_rows(const osc_model* model, int32_t* rows);
 
 /* osc_batch_solve with the per-call extras (NULL extras = osc_batch_solve).  A model with wheel
- * rows is solved only through this entry (and osc_batch_assemble_ex + osc_batch_solve_assembled);
- * its warm-started and multi-model paths return OSC_ERR_UNSUPPORTED_DIMS. */
+ * rows is solved through this entry, osc_batch_solve_warm_ex, or osc_batch_assemble_ex followed
+ * by osc_batch_solve_assembled(_warm); its multi-model path returns OSC_ERR_UNSUPPORTED_DIMS. */
 int osc_batch_solve_ex(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask, const osc_solve_extras* extras,
                        double* tau, double* x, int32_t* status, int32_t* iters,
                        void* workspace, size_t workspace_bytes, void* stream);
+/* osc_batch_solve_warm with the per-call extras (wheel directions, duals): the warm-started tick
+ * of a wheel-row model (the reference's walter_sr_wheels controller warm-starts every tick,
+ * walter_sr_wheels/operational_space_controller.h:583, 591-600). */
+int osc_batch_solve_warm_ex(const osc_model* model, int32_t nenv,
+                            const double* M, const double* C, const double* J, const double* b,
+                            const double* T, const double* contact_mask,
+                            const osc_solve_extras* extras, double* tau, double* x,
+                            int32_t* status, int32_t* iters, double* warm_state,
+                            size_t warm_state_bytes, void* workspace, size_t workspace_bytes,
+                            void* stream);
 int osc_batch_assemble_ex(const osc_model* model, int32_t nenv,
                           const double* M, const double* C, const double* J, const double* b,
                           const double* T, const double* contact_mask, const double* wheel_dir,

@@ -77,7 +77,6 @@ struct DevParams {
   double wheel_radius[OSC_MAX_SITES];
   double wheel_tol;                  // interior point: |row residual| <= wheel_tol to stop
   double refine_max_move;            // a refinement moving y by more (relative) is rejected
-  int32_t refine_dual_extra;         // WH with duals requested: this many more refinement steps
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -1459,11 +1458,10 @@ __device__ __forceinline__ void ipm_block(
   // run (cold, from the same workspace); only those envs' outputs are rewritten.
   bool write_out = valid;
   if constexpr (WARM) {
-    // (not an env the warm pass converged whose refinement was rejected, OSC_SOLVE_UNREFINED: a
-    // cold solve rejects the same refinement -- measured on the joint-state control loop, where
-    // redoing them cost a cold wavefront per tick, tools/warm_qpos_status.py)
-    const bool redo = valid && fixup && gstatus[env] != OSC_SOLVE_OK &&
-                      gstatus[env] != OSC_SOLVE_UNREFINED;
+    // (an env whose refinement found no KKT point, OSC_SOLVE_UNREFINED, too: the warm start can
+    // leave the interior point's early stop with an active set the refinement cannot repair,
+    // ~1 env in 4,096 x 10 joint-state ticks; the cold fix-up solve runs to mu <= 1e-12)
+    const bool redo = valid && fixup && gstatus[env] != OSC_SOLVE_OK;
     if (fixup && __ballot(redo) == 0) return;
     write_out = valid && (!fixup || redo);
   }
@@ -1892,6 +1890,29 @@ __device__ __forceinline__ void ipm_block(
     return PA.park_it;
   };
   bool parked = false;   // park pass: this row's env went to the park area (no outputs here)
+  bool refined = false;
+  // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
+  // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
+  // every other multiplier from the design vector itself.
+  // (w = L' nu: the multipliers of the rows [V X | V x0 - vs] before their orthonormalisation,
+  // which the dual kernel maps back to E's rows; every lane of the env's row takes part)
+  auto put_wheel_duals = [&](double nu) {
+    if constexpr (D::WH) {
+      if (want_dual) {
+        const double* Lw = ws + static_cast<size_t>(env) * D::WS + D::W_WL;
+        const int lc = l < NW ? l : 0;
+        double acc = 0.0;
+        static_for<0, NW>([&](auto W) {
+          constexpr int w = decltype(W)::value;
+          acc = fma(Lw[w * NW + lc], bcast_guarded<w>(nu), acc);
+        });
+        if (write_out && l < NW)
+          const_cast<double*>(ws)[static_cast<size_t>(env) * D::WS + D::W_NU + l] = acc;
+      }
+    }
+  };
+  // interior-point stop (the warm fix-up pass is a rescue: its cold solve runs to mu <= 1e-12)
+  const double eps_run = (WARM && fixup) ? fmin(P->eps_mu, 1e-12) : P->eps_mu;
   if constexpr (REFINE) {
     // the interior point's result for this env (osc_ipm_kernel, W_SOL): y, and the active rows
     // as lambda > s with lambda = q > 0
@@ -1956,6 +1977,15 @@ __device__ __forceinline__ void ipm_block(
           }
         }
       }
+      if constexpr (WHR) {
+        // the wheel rows' residual at the warm y (this tick's rows: directions and mask are new
+        // every tick; the first Newton step's pinned coordinates step onto them exactly)
+        double yh0, yh1;
+        rot_in(y0, y1, yh0, yh1);
+        rq0 = pin0 ? yh0 + q10 : 0.0;
+        rq1 = pin1 ? yh1 + q11 : 0.0;
+        rwmax = row_max(fmax(fabs(rq0), fabs(rq1)));
+      }
     }
     // An env still far from converged (mu > 1e-6) at iteration `restart_iter` (warm-started:
     // `warm_restart`) is re-centred in place -- slacks h - G y + 1, multipliers 1: the cold
@@ -1996,7 +2026,7 @@ __device__ __forceinline__ void ipm_block(
           rp[t] = fresh ? r : rp[t];
         }
       }
-      if (!done && mu <= P->eps_mu && (!D::WH || rwmax <= P->wheel_tol)) {
+      if (!done && mu <= eps_run && (!D::WH || rwmax <= P->wheel_tol)) {
         done = true;
         st = OSC_SOLVE_OK;
         it_done = it;
@@ -2261,30 +2291,9 @@ __device__ __forceinline__ void ipm_block(
   // (tools/ipm_model.py + the refinement study in DESIGN.md).  Envs that did not converge keep
   // their iterate; a refinement that moves y by more than 1e-3 (relative) or is not finite is
   // discarded.
-  bool refined = false;
-  if constexpr (CP == kCpPark) write_out = write_out && !parked;   // the resume pass writes them
-  // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
-  // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
-  // every other multiplier from the design vector itself.
-  // (w = L' nu: the multipliers of the rows [V X | V x0 - vs] before their orthonormalisation,
-  // which the dual kernel maps back to E's rows; every lane of the env's row takes part)
-  auto put_wheel_duals = [&](double nu) {
-    if constexpr (D::WH) {
-      if (want_dual) {
-        const double* Lw = ws + static_cast<size_t>(env) * D::WS + D::W_WL;
-        const int lc = l < NW ? l : 0;
-        double acc = 0.0;
-        static_for<0, NW>([&](auto W) {
-          constexpr int w = decltype(W)::value;
-          acc = fma(Lw[w * NW + lc], bcast_guarded<w>(nu), acc);
-        });
-        if (write_out && l < NW)
-          const_cast<double*>(ws)[static_cast<size_t>(env) * D::WS + D::W_NU + l] = acc;
-      }
-    }
-  };
-  // the duals ask the refinement for more steps (its multipliers converge more slowly than y)
-  const int refine_steps = P->refine_steps + ((D::WH && want_dual) ? P->refine_dual_extra : 0);
+  // (wheel rows: a fixed step count, the same whether or not the duals are asked for, so x and tau
+  // do not depend on want_dual -- the rows' multipliers converge more slowly than y, hence 12)
+  const int refine_steps = P->refine_steps;
   if constexpr (RF != kRfNone) {
     // WH: an env the interior point left at max_iter is refined too (its rotated Newton systems
     // can stall short of eps_mu with the active set already right): a kept refinement -- no row
@@ -2618,6 +2627,10 @@ __device__ __forceinline__ void ipm_block(
           for (int t = 0; t < NRL; ++t) {
             const bool leave = Dr[t] != 0.0 && mur[t] < -mtol;
             Dr[t] = leave ? 0.0 : Dr[t];
+            // (its multiplier leaves with it: the residual sums G'mu over every row slot, and a
+            // stale negative multiplier there would move the next round's fixed point off the
+            // optimum while no test looks at that row any more)
+            mur[t] = leave ? 0.0 : mur[t];
             nviol += leave ? 1.0 : 0.0;
           }
         }
@@ -3064,7 +3077,8 @@ int ww_doubles(KernelId k) {
   switch (k) {
     case K_GO2: return Go2::WW;
     case K_WALTER: return Walter::WW;
-    default: return 0;   // (no warm start with wheel rows)
+    case K_WALTER_WHEELS: return WalterW::WW;
+    default: return 0;
   }
 }
 
@@ -3136,9 +3150,9 @@ void tuning_defaults(const osc_model_desc& d, osc_model_tuning& t) {
   std::memset(&t, 0, sizeof(t));
   // full-space refinement: at least two steps per round with one factorisation,
   // each env until its own step converges (numpy model: <= 3e-12 normwise on Go2 / WaLTER
-  // batches, from up to 2e-2 without it); wheel rows: eight, run to convergence from the interior
-  // point's earlier stop
-  t.refine_steps = d.wheel_rows ? 8 : 2;
+  // batches, from up to 2e-2 without it); wheel rows: twelve, run to convergence (the rows'
+  // multipliers, exported as duals, converge more slowly than y)
+  t.refine_steps = d.wheel_rows ? 12 : 2;
   t.refine_max_move = 1e300;
   t.eps_mu = d.eps_mu;
   // warm start (round 3, profiles/r03_warm_settings.txt: delta 0.1 -> 1 and
@@ -3252,9 +3266,8 @@ extern "C" int osc_model_create_tuned(const osc_model_desc* desc, const osc_mode
   hp.refine_steps = t.refine_steps;
   hp.refine_penalty = 1e2;   // active-row penalty of the refinement, x max diag(Hr)
   hp.refine_max_move = t.refine_max_move;
-  hp.refine_dual_extra = 4;
-  // The YAML's Go2 stop (eps_mu 1e-9) presumes the refinement finishes the solve; without it the
-  // interior point runs to 1e-12 itself.
+  // The early stops (Go2 1e-6, WaLTER 1e-8: osc_desc_from_yaml) presume the refinement finishes
+  // the solve; without it the interior point runs to 1e-12 itself.
   if (hp.refine_steps <= 0) hp.eps_mu = std::fmin(hp.eps_mu, 1e-12);
   for (int i = 0; i < OSC_MAX_SITES; ++i) hp.wheel_dof[i] = -1;
   for (int i = 0; d.wheel_rows && i < d.nc; ++i) {
@@ -3349,9 +3362,19 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
   const unsigned nb = static_cast<unsigned>((nenv + kEnvPerWave - 1) / kEnvPerWave);
   const int flags = y != nullptr ? 2 : 0;   // hand the multipliers to the dual kernel
   if constexpr (D::WH) {
-    // wheel rows: the cold one-wave solve with the refinement fused (launch() checked the rest)
-    hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                       model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
+    // wheel rows: the one-wave solve with the refinement fused (launch() checked the rest); warm-
+    // started: the warm pass, then the cold fix-up pass over the wavefronts holding an env the
+    // warm start left unconverged (the per-env status: the caller's array, else scratch)
+    if (warm == nullptr) {
+      hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                         model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
+    } else {
+      if (status == nullptr) status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
+      for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, warm,
+                           flags | pass);
+    }
   } else {
     // A warm-started solve is followed by a cold fix-up pass over the wavefronts that hold an
     // env the warm start did not bring to convergence (it needs the per-env status: the
@@ -3454,7 +3477,6 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
     return OSC_ERR_INVALID_ARGUMENT;   // 16-byte alignment: vectorised staging loads
   if ((stages & kInteriorPoint) && !tau) return OSC_ERR_INVALID_ARGUMENT;
   const bool wheels = model->kid == K_WALTER_WHEELS;
-  if (wheels && warm != nullptr) return OSC_ERR_UNSUPPORTED_DIMS;   // no warm start with them
   if (wheels && (stages & kAssemble) && wdir == nullptr) return OSC_ERR_INVALID_ARGUMENT;
   if (y != nullptr && (x == nullptr || (stages & kBoth) != kBoth)) return OSC_ERR_INVALID_ARGUMENT;
   if (y != nullptr && !model->refine) return OSC_ERR_INVALID_ARGUMENT;   // (fused path only)
@@ -3627,6 +3649,20 @@ extern "C" int osc_batch_solve_warm(const osc_model* model, int32_t nenv, const 
   if (!warm_small(model, nenv, warm_state, warm_state_bytes)) return OSC_ERR_INVALID_ARGUMENT;
   return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
                 workspace_bytes, stream, kBoth, warm_state);
+}
+
+extern "C" int osc_batch_solve_warm_ex(const osc_model* model, int32_t nenv, const double* M,
+                                       const double* C, const double* J, const double* b,
+                                       const double* T, const double* contact_mask,
+                                       const osc_solve_extras* extras, double* tau, double* x,
+                                       int32_t* status, int32_t* iters, double* warm_state,
+                                       size_t warm_state_bytes, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  if (!warm_small(model, nenv, warm_state, warm_state_bytes)) return OSC_ERR_INVALID_ARGUMENT;
+  const double* wdir = extras ? extras->wheel_dir : nullptr;
+  if (wdir && misaligned16(wdir)) return OSC_ERR_INVALID_ARGUMENT;
+  return launch(model, nenv, M, C, J, b, T, contact_mask, tau, x, status, iters, workspace,
+                workspace_bytes, stream, kBoth, warm_state, wdir, extras ? extras->y : nullptr);
 }
 
 extern "C" int osc_batch_solve_assembled_warm(const osc_model* model, int32_t nenv,

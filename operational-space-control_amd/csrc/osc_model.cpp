@@ -214,11 +214,16 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   desc->z_lb[0] = -inf; desc->z_lb[1] = -inf; desc->z_lb[2] = 0.0;
   desc->z_ub[0] = inf;  desc->z_ub[1] = inf;  desc->z_ub[2] = big_number;
   desc->infinity = inf;
-  // interior-point stop.  The full-space refinement that follows (osc_batch.hip) needs only the
-  // active set identified: Go2 stops at 1e-9 (GPU, 32,768-env batches with refinement: worst
-  // normwise error vs the exact optimum 4e-12 standing, ~1e-11 tumbling; -1.5 iterations),
-  // WaLTER at 1e-12 (at 1e-9 its degenerate contact rows are not yet resolved; numpy model)
-  desc->eps_mu = std::strcmp(robot, "unitree_go2") == 0 ? 1e-9 : 1e-12;
+  // interior-point stop.  The full-space refinement that follows (osc_batch.hip) needs only an
+  // approximate active set: its rounds add the rows its point violates and drop the rows whose
+  // multiplier comes out negative, and it is kept only at a KKT point.  So the
+  // interior point stops early -- Go2 at 1e-6, WaLTER at 1e-8 (numpy model of the kernel,
+  // tools/kkt_study.py, 1,024-env synthetic and joint-state batches: no rejection, worst error
+  // vs the exact optimum 1e-11; slowest wave of four envs -1.5 (Go2) / -2.0 (WaLTER) iterations
+  // for +0.0-0.7 (Go2) / +0.5-1.4 (WaLTER) refinement steps against 1e-9 / 1e-12).  The opt-in
+  // wheel rows keep 1e-12: their rotated Newton systems stop on their own stall test
+  // (DESIGN.md §3.1), and their refinement's acceptance bounds were set around that stop.
+  desc->eps_mu = std::strcmp(robot, "unitree_go2") == 0 ? 1e-6 : 1e-8;   // (wheel rows: below)
   desc->max_iter = 50;   // normal solves take <= 24; the margin covers a re-centred stall
   // optional wheel no-slip rows (walter_sr_wheels/autogen/autogen.py:128-240, commented out
   // upstream): `wheel_no_slip: true`, `wheel_radius: r` (or one per wheel, the design's 0.065 at
@@ -227,6 +232,7 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   const std::string& ns_flag = y.scalars["wheel_no_slip"];
   if (ns_flag == "true" || ns_flag == "True" || ns_flag == "1") {
     desc->wheel_rows = 1;
+    desc->eps_mu = 1e-12;   // the wheel rows' interior point keeps the late stop (above)
     const auto& rl = y.lists["wheel_radius"];
     double r = 0.0;
     const bool scalar_r = rl.empty() && to_double(y.scalars["wheel_radius"], &r);

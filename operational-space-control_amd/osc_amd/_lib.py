@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_contact_geom_table", "osc_tumbling_params_default",
                     "osc_tumbling_targets", "osc_dual_rows", "osc_batch_solve_ex",
                     "osc_batch_assemble_ex", "osc_model_tuning_defaults",
-                    "osc_model_create_tuned")
+                    "osc_model_create_tuned", "osc_batch_solve_warm_ex")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -177,6 +177,9 @@ def lib() -> ctypes.CDLL:
     L.osc_batch_solve_warm.argtypes = [vp, i32] + [vp] * 11 + [ctypes.c_size_t, vp,
                                                                ctypes.c_size_t, vp]
     L.osc_batch_solve_warm.restype = ctypes.c_int
+    L.osc_batch_solve_warm_ex.argtypes = [vp, i32] + [vp] * 6 + [ctypes.POINTER(OscSolveExtras)] + \
+        [vp] * 5 + [ctypes.c_size_t, vp, ctypes.c_size_t, vp]
+    L.osc_batch_solve_warm_ex.restype = ctypes.c_int
     L.osc_batch_solve_assembled_warm.argtypes = [vp, i32] + [vp] * 6 + [ctypes.c_size_t, vp,
                                                                          ctypes.c_size_t, vp]
     L.osc_batch_solve_assembled_warm.restype = ctypes.c_int

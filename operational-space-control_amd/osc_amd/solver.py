@@ -180,12 +180,25 @@ class OSCBatchSolver:
         return torch.zeros((max(nb.value // 8, 2),), dtype=torch.float64, device=self.device)
 
     def solve_warm_into(self, out: SolveResult, warm: torch.Tensor, M, C, J, b, T, mask,
-                        stream=None) -> SolveResult:
+                        stream=None, wheel_dir=None) -> SolveResult:
         """osc_batch_solve_warm: as solve_into, starting from (and updating) `warm`, the previous
-        tick's solution (the reference's SetWarmStart, operational_space_controller.h:519-526)."""
+        tick's solution (the reference's SetWarmStart, operational_space_controller.h:519-526);
+        osc_batch_solve_warm_ex with wheel rows or duals (out.y)."""
         nenv = out.tau.shape[0]
         s = (torch.cuda.current_stream(self.device) if stream is None else stream).cuda_stream
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        if wheel_dir is not None or out.y is not None:
+            ex = _lib.OscSolveExtras(wheel_dir.data_ptr() if wheel_dir is not None else None,
+                                     out.y.data_ptr() if out.y is not None else None)
+            rc = _lib.lib().osc_batch_solve_warm_ex(
+                self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T), ptr(mask),
+                ctypes.byref(ex), ptr(out.tau), ptr(out.x), ptr(out.status), ptr(out.iters),
+                ptr(warm), ctypes.c_size_t(warm.numel() * 8), ptr(out.workspace),
+                ctypes.c_size_t(0 if out.workspace is None else out.workspace.numel() * 8),
+                ctypes.c_void_p(s))
+            if rc != 0:
+                raise _lib.OSCError("osc_batch_solve_warm_ex", rc)
+            return out
         rc = _lib.lib().osc_batch_solve_warm(self._h, nenv, ptr(M), ptr(C), ptr(J), ptr(b), ptr(T),
                                              ptr(mask), ptr(out.tau), ptr(out.x), ptr(out.status),
                                              ptr(out.iters), ptr(warm),

@@ -164,10 +164,11 @@ def _kkt_solve(K, rhs):
     return np.linalg.lstsq(K, rhs, rcond=None)[0]
 
 
-def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
-                refine_steps: int = 4) -> ExactSolution:
+def _primal_active_set(model: OSCModel, qp: QPData, M, C, J, eq, ineq, max_iter: int):
+    """Primal active-set method (Nocedal & Wright, Alg. 16.3) from a strictly feasible point.
+    Returns the working set (indices into ineq) and the iteration count; RuntimeError when it
+    cycles past max_iter (degenerate working sets of the wheel rows)."""
     n = model.n
-    eq, ineq = _constraints(qp)
     A = qp.A
     x = (_feasible_start(model, qp, M, C, J) if qp.Aw is None else _phase1_start(qp, eq, ineq))
     # sanity: strictly feasible for all one-sided rows
@@ -224,10 +225,109 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
             W.append(block)
     else:
         raise RuntimeError("active set did not converge")
+    return W, it
 
-    # Final exact KKT solve on the identified active set (removes accumulated step rounding).
+
+def _dual_active_set(qp: QPData, eq, ineq, max_iter: int = 5000):
+    """Goldfarb & Idnani's dual active-set method (Math. Programming 27, 1983; the algorithm of
+    quadprog) for the strictly convex QP: start at the unconstrained minimiser, add the equality
+    rows, then repeatedly the most violated one-sided row, keeping the working set's multipliers
+    non-negative.  A row linearly dependent on the working set is never added: a pure dual step
+    first drops a working row (the degenerate pyramid apex; dependent wheel rows).  Every iterate
+    is dual feasible and the dual objective rises strictly, so it terminates without the primal
+    method's cycling.  Returns the working set (indices into ineq) and the iteration count.
+    Rows as normals c'x >= b: a one-sided row sg a_i x <= bd is (-sg a_i) x >= -bd.
+    (J, R recomputed per step by a QR of L^-T' N: n <= 46, cheap, no update formulas to get
+    wrong.)"""
+    import scipy.linalg as sla
+    H, f, A = qp.H, qp.f, qp.A
+    n = H.shape[0]
+    Lc = np.linalg.cholesky(H)
+    J0 = sla.solve_triangular(Lc, np.eye(n), lower=True).T          # L^-T: J0 J0' = H^-1
+    x = -np.linalg.solve(H, f)
+    normals = [A[i] for i in eq] + [-sg * A[i] for (i, sg, _) in ineq]
+    rhs = [qp.u[i] for i in eq] + [-bd for (_, _, bd) in ineq]
+    neq = len(eq)
+    act: list[int] = []               # indices into normals
+    u = np.zeros(0)
+
+    def factor():
+        q = len(act)
+        if q == 0:
+            return J0, np.zeros((0, 0))
+        Q, R = np.linalg.qr(J0.T @ np.column_stack([normals[k] for k in act]), mode="complete")
+        return J0 @ Q, R[:q, :q]
+
+    def step_dirs(c):
+        J, R = factor()
+        q = len(act)
+        d = J.T @ c
+        z = J[:, q:] @ d[q:]
+        r = sla.solve_triangular(R, d[:q]) if q else np.zeros(0)
+        return z, r
+
+    scale_c = [np.abs(c).max() for c in normals]
+    it = 0
+    for k in range(neq):              # equality rows: always active, multipliers of any sign
+        c = normals[k]
+        z, r = step_dirs(c)
+        if np.abs(z).max() <= 1e-13 * scale_c[k]:
+            continue                  # implied by the rows already in (consistent by construction)
+        t = (rhs[k] - c @ x) / (z @ c)
+        x = x + t * z
+        u = np.append(u - t * r, t)
+        act.append(k)
+    while True:
+        it += 1
+        if it > max_iter:
+            raise RuntimeError("dual active set did not converge")
+        xs = np.abs(x).max()
+        s = np.array([normals[k] @ x - rhs[k] for k in range(neq, len(normals))])
+        viol = s / (1.0 + np.array(scale_c[neq:]) * xs + np.abs(rhs[neq:]))
+        p = neq + int(np.argmin(viol)) if len(s) else None
+        if p is None or viol[p - neq] >= -1e-14 or p in act:
+            break
+        c = normals[p]
+        up = np.append(u, 0.0)
+        while True:
+            z, r = step_dirs(c)
+            q = len(act)
+            t1, kdrop = np.inf, None
+            for j in range(q):
+                if act[j] >= neq and r[j] > 1e-14 * (1.0 + np.abs(r).max()):
+                    ratio = up[j] / r[j]
+                    if ratio < t1:
+                        t1, kdrop = ratio, j
+            dependent = np.abs(z).max() <= 1e-13 * scale_c[p] * (1.0 + np.abs(J0).max())
+            t2 = np.inf if dependent else -(c @ x - rhs[p]) / (z @ c)
+            t = min(t1, t2)
+            if not np.isfinite(t):
+                raise RuntimeError("QP infeasible (dual unbounded)")
+            if not dependent:
+                x = x + t * z
+            up[:q] -= t * r
+            up[q] += t
+            if t2 <= t1:              # full step: p joins the working set
+                act.append(p)
+                u = up
+                break
+            del act[kdrop]            # partial step: a working row whose multiplier hit 0 leaves
+            up = np.delete(up, kdrop)
+            if not dependent and c @ x - rhs[p] >= 0.0:
+                u = up[:-1]           # (p satisfied without joining: cannot happen for t < t2)
+                break
+    return [k - neq for k in act if k >= neq], it
+
+
+def _finish(model: OSCModel, qp: QPData, eq, ineq, W, it, refine_steps: int) -> ExactSolution:
+    """Exact KKT solve on the identified working set W, polished by mixed-precision iterative
+    refinement, with the multipliers mapped to OSQP's convention and the KKT certificate."""
+    n = model.n
+    A = qp.A
+    Aeq = A[eq]
+    neq = Aeq.shape[0]
     rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
-    rhs_b = np.concatenate([beq] + [[ineq[w][2]] for w in W]) if W else beq
+    rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
     k = rows.shape[0]
     K = np.zeros((n + k, n + k))
     K[:n, :n] = qp.H
@@ -261,6 +361,23 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
         active[i] = True
     cert = kkt_certificate(qp, x, y)
     return ExactSolution(x=x, y=y, active=active, iterations=it, cert=cert)
+
+
+def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
+                refine_steps: int = 4, method: str = "auto") -> ExactSolution:
+    """The QP's unique optimum with its KKT certificate.  method "primal": the primal active-set
+    method; "dual": Goldfarb-Idnani; "auto": primal, and the dual method where the primal one
+    cycles or ends on an inconsistent degenerate working set (a few wheel-row envs)."""
+    eq, ineq = _constraints(qp)
+    if method in ("primal", "auto"):
+        try:
+            W, it = _primal_active_set(model, qp, M, C, J, eq, ineq, max_iter)
+            return _finish(model, qp, eq, ineq, W, it, refine_steps)
+        except RuntimeError:
+            if method == "primal":
+                raise
+    W, it = _dual_active_set(qp, eq, ineq)
+    return _finish(model, qp, eq, ineq, W, it, refine_steps)
 
 
 def certified(cert: dict, tol: float = 1e-9) -> bool:

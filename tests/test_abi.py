@@ -35,7 +35,7 @@ def test_tuning_defaults(robot):
     d = _lib.desc_from_yaml(robot)
     t = _lib.OscModelTuning()
     assert L.osc_model_tuning_defaults(ctypes.byref(d), ctypes.byref(t)) == 0
-    assert t.refine_steps == (8 if d.wheel_rows else 2)
+    assert t.refine_steps == (12 if d.wheel_rows else 2)
     assert t.refine_max_move == 1e300 and t.eps_mu == d.eps_mu
     assert (t.restart_iter, t.warm_restart, t.warm_delta, t.warm_center) == (28, 22, 1.0, 1.0)
     assert t.wheel_tol == 1e-6 and t.small_batch_max == -1 and t.park_it == -1

@@ -99,21 +99,17 @@ def test_wheel_rows_vs_oracle(gpu, scenario, mask_mode, seed):
     ok_frac = WHEEL_OK_FRAC[scenario]
     assert (st == 0).mean() >= ok_frac, np.bincount(st)
     x = res.x.cpu().numpy()
-    ref, viol, envs, no_oracle = [], [], [], []
+    ref, viol, envs = [], [], []
     for e in range(nenv):
         if st[e] != 0:
             continue
         args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *args, wheel, wd[e])
         viol.append(np.abs(qp.Aw @ x[e] - qp.bw).max() / (1.0 + np.abs(qp.bw).max()))
-        try:
-            ref.append(torque(model, solve_exact(model, qp, *args[:3]).x))
-            envs.append(e)
-        except RuntimeError:
-            # the active-set oracle refuses a few degenerate envs (qp_exact.solve_exact); the GPU
-            # result of every env is still held to the rows here and to the KKT certificate below
-            no_oracle.append(e)
-    assert len(no_oracle) <= nenv // 16, no_oracle
+        # (the oracle's dual active-set method takes the degenerate envs the primal one refuses:
+        # every env is checked)
+        ref.append(torque(model, solve_exact(model, qp, *args[:3]).x))
+        envs.append(e)
     nw, el = _rel_errors(res.tau.cpu().numpy()[envs], np.array(ref))
     assert nw.max() <= WHEEL_NORM and el.max() <= WHEEL_ELEM, (nw.max(), el.max(), int(np.argmax(nw)))
     assert np.median(nw) <= WHEEL_MEDIAN, np.median(nw)
@@ -138,8 +134,8 @@ def test_wheel_rows_that_vanish_change_nothing(gpu, tmp_path):
 
 
 def test_wheel_model_entry_points(gpu):
-    """A wheel model needs its directions: the plain entries refuse it, warm start and the
-    multi-model call are not compiled for it, split assemble + solve equals the fused call."""
+    """A wheel model needs its directions: the plain entries (cold and warm) refuse it, split
+    assemble + solve equals the fused call."""
     from osc_amd import _lib
     s = solver("noslip")
     d = generate("walter_sr_wheels", 8, SEED_BASE + 84, "tumbling", "bernoulli")
@@ -153,7 +149,7 @@ def test_wheel_model_entry_points(gpu):
     warm = s.alloc_warm_state(8)
     with pytest.raises(_lib.OSCError) as e:
         s.solve_warm_into(out, warm, *args)
-    assert e.value.code == 2
+    assert e.value.code == 1
     s.solve_into(out, *args, wheel_dir=wd)
     split = s.alloc_outputs(8, want_x=True)
     s.assemble_into(split, *args[:5], args[5], wheel_dir=wd)
@@ -304,7 +300,7 @@ def test_wheel_rows_kkt_certificate(gpu):
 def test_rejected_refinement_is_reported(gpu):
     """An env whose full-space refinement is rejected keeps the interior point's iterate and is
     reported as OSC_SOLVE_UNREFINED (3), not OK; its torques are only as accurate as the
-    interior point's stop (Go2 eps_mu 1e-9: ~1e-5 normwise)."""
+    interior point's stop (Go2 eps_mu 1e-6: up to ~1e-2 normwise)."""
     from osc_amd.solver import OSCBatchSolver
     # every refinement moves y: all rejected
     s = OSCBatchSolver("unitree_go2", tuning={"refine_max_move": 0.0})
@@ -316,4 +312,59 @@ def test_rejected_refinement_is_reported(gpu):
     assert (st == 3).all(), np.bincount(st)
     assert (good.status.cpu().numpy() == 0).all()
     nw, _ = _rel_errors(res.tau.cpu().numpy(), good.tau.cpu().numpy())
-    assert nw.max() <= 1e-4 and nw.max() > 0.0, nw.max()
+    assert nw.max() <= 3e-2 and nw.max() > 0.0, nw.max()
+
+
+def test_wheel_duals_leave_primal_unchanged(gpu):
+    """Asking for the duals (osc_solve_extras.y) does not change the wheel model's solve: x, tau,
+    status and iters are bitwise those of the call without them (the refinement runs the same
+    fixed step count either way)."""
+    wheel = _wheel()
+    s = solver("noslip")
+    nenv = 512
+    d = generate("walter_sr_wheels", nenv, SEED_BASE + 90, "tumbling", "bernoulli")
+    wdt = torch.from_numpy(wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius,
+                                            SEED_BASE + 91)).cuda()
+    args = s.prepare(**d)
+    a = s.alloc_outputs(nenv, want_y=True)
+    s.solve_into(a, *args, wheel_dir=wdt)
+    b = s.alloc_outputs(nenv, want_x=True)
+    s.solve_into(b, *args, wheel_dir=wdt)
+    torch.cuda.synchronize()
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+@pytest.mark.parametrize("scenario,mask_mode", [("standing", "ones"), ("tumbling", "bernoulli")])
+def test_wheel_rows_warm_start(gpu, scenario, mask_mode):
+    """Warm start with the wheel rows (osc_batch_solve_warm_ex; the reference's wheels controller
+    warm-starts every tick, walter_sr_wheels/operational_space_controller.h:583, 591-600): five
+    ticks of a 1 % random walk of the inputs (the wheel directions follow), masks fixed.  Every tick's
+    warm solve agrees with the cold solve of the same tick to the wheel rows' tolerance, reports
+    the same statuses, and takes fewer interior-point iterations on average after the first."""
+    from osc_amd.synth import random_walk
+    wheel = _wheel()
+    s = solver("noslip")
+    nenv = 1024
+    d = generate("walter_sr_wheels", nenv, SEED_BASE + 95, scenario, mask_mode)
+    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + 96)
+    rng = np.random.default_rng(7)
+    warm = s.alloc_warm_state(nenv)
+    wo, co = s.alloc_outputs(nenv), s.alloc_outputs(nenv)
+    for tick in range(5):
+        args = s.prepare(**d)
+        wdt = torch.from_numpy(wd).cuda()
+        s.solve_warm_into(wo, warm, *args, wheel_dir=wdt)
+        s.solve_into(co, *args, wheel_dir=wdt)
+        torch.cuda.synchronize()
+        sw, sc = wo.status.cpu().numpy(), co.status.cpu().numpy()
+        ok = (sw == 0) & (sc == 0)
+        assert ok.mean() >= (1.0 if scenario == "standing" else 0.98), (tick, np.bincount(sw), np.bincount(sc))
+        nw, _ = _rel_errors(wo.tau.cpu().numpy()[ok], co.tau.cpu().numpy()[ok])
+        assert nw.max() <= WHEEL_NORM, (tick, nw.max())
+        if tick > 0:
+            assert wo.iters.float().mean() < co.iters.float().mean(), tick
+        d = random_walk(d, rng)
+        # (directions re-derived from the walked state with the same seed: they move continuously
+        # and stay consistent -- eight grounded wheels put 16 rows on 14 accelerations)
+        wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, SEED_BASE + 96)

@@ -233,3 +233,42 @@ def test_wheel_qp_exact_optimum_certified():
         assert np.abs(qp.Aw @ sol.x - qp.bw).max() <= 1e-9 * (1 + np.abs(qp.bw).max())
         free = solve_exact(model, build_qp(model, *args), *args[:3])
         assert np.abs(torque(model, free.x) - torque(model, sol.x)).max() > 1e-3
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_dual_active_set_agrees_with_primal(path):
+    """The oracle's two exact methods -- the primal active-set method and Goldfarb-Idnani's dual
+    one (qp_exact._dual_active_set) -- share no iteration logic; on every golden env they return
+    the same optimum to 1e-12 and both certify."""
+    g = _load(path)
+    model = load_model(str(g["robot"]))
+    wheel = None
+    if "wheel_dir" in g:
+        model, wheel = _wheel_setup()
+    for e in range(g["M"].shape[0]):
+        args = _args(g, e)
+        qp = build_qp(model, *args, *((wheel, g["wheel_dir"][e]) if wheel is not None else ()))
+        a = solve_exact(model, qp, *args[:3], method="primal")
+        b = solve_exact(model, qp, *args[:3], method="dual")
+        assert certified(b.cert), b.cert
+        assert np.abs(a.x - b.x).max() <= 1e-12 * (1 + np.abs(a.x).max())
+
+
+def test_dual_active_set_takes_degenerate_wheel_envs():
+    """Wheel-row tumbling envs on which the primal active-set method cycles (Bland's rule does not
+    resolve every dependent working set: 'active set did not converge') or ends on an inconsistent
+    degenerate set: the dual method certifies each at 1e-9 and solve_exact ("auto") returns that
+    solution -- the oracle now accepts every env of the wheel census (4 seeds x 2,048 envs,
+    DESIGN.md §2)."""
+    from osc_amd.synth import SEED_BASE, generate, wheel_directions
+    model, wheel = _wheel_setup()
+    d = generate(model.name, 2048, SEED_BASE + 82, "tumbling", "bernoulli")   # (the census batch)
+    wd = wheel_directions(model.name, d, wheel.dof, wheel.radius, SEED_BASE + 83)
+    for e in (178, 665, 1436):
+        args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        qp = build_qp(model, *args, wheel, wd[e])
+        with pytest.raises(RuntimeError):
+            solve_exact(model, qp, *args[:3], method="primal")
+        sol = solve_exact(model, qp, *args[:3])
+        assert certified(sol.cert), (e, sol.cert)
+        assert np.abs(qp.Aw @ sol.x - qp.bw).max() <= 1e-9 * (1 + np.abs(qp.bw).max())

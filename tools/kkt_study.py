@@ -185,19 +185,20 @@ def refine_new(Hr, G, h, resid, y, s, lam, pen=1e2, steps_min=2, steps_max=8, ro
     return ya, False, info
 
 
-def sweep(robot="unitree_go2", nenv=1024, jr=0.5, so=7, synth=False, **kw):
+def sweep(robot="unitree_go2", nenv=1024, jr=0.5, so=7, synth=False, eps=1e-9, oracle=True, **kw):
     """IPM (numpy model) + refine_new over a joint-state batch: failures and worst error."""
     import ipm_model
     seed = shard_seed(0) + so
     model = load_model(robot)
     nv, nu = model.nv, model.nu
     if synth:
-        dd = generate(robot, nenv, seed, "tumbling", "bernoulli")
+        dd = generate(robot, nenv, seed, *((synth.split(",")) if isinstance(synth, str)
+                                            else ("tumbling", "bernoulli")))
     else:
         km = okin.load(robot)
         qpos, qvel = random_states(load_tree(robot), nenv, seed, joint_range=jr)
         dd = generate(robot, nenv, seed, "standing", "ones")
-    worst, nfail, nref, steps, rounds = 0.0, 0, 0, [], []
+    worst, nfail, nref, steps, rounds, its = 0.0, 0, 0, [], [], []
     t0 = time.time()
     for e in range(nenv):
         if synth:
@@ -207,7 +208,8 @@ def sweep(robot="unitree_go2", nenv=1024, jr=0.5, so=7, synth=False, **kw):
         args = (M, C, J, b, dd["T"][e], dd["mask"][e])
         qp = build_qp(model, *args)
         Hr, g, G, h, P, p0 = reduce_qp_tau(model, *args)
-        y, it, st = ipm(Hr, g, G, h, eps_mu=1e-9, max_iter=50)[:3]
+        y, it, st = ipm(Hr, g, G, h, eps_mu=eps, max_iter=50)[:3]
+        its.append(it)
         s, lam = ipm_model.FINAL["s"], ipm_model.FINAL["lam"]
         X, x0 = P[:nv], p0[:nv]
         Hd, fd = qp.H[:nv, :nv], qp.f[:nv]
@@ -217,6 +219,9 @@ def sweep(robot="unitree_go2", nenv=1024, jr=0.5, so=7, synth=False, **kw):
             return X.T @ (Hd @ (X @ yv + x0) + fd) + wdiag * yv
         ya, ok, info = refine_new(Hr, G, h, resid, y, s, lam, **kw)
         steps.append(info["steps"]); rounds.append(info["rounds"])
+        if not oracle:
+            nfail += 0 if ok else 1
+            continue
         try:
             ex = solve_exact(model, qp, M, C, J)
         except Exception:
@@ -233,4 +238,9 @@ def sweep(robot="unitree_go2", nenv=1024, jr=0.5, so=7, synth=False, **kw):
             worst = max(worst, err)
     print(f"{robot} jr {jr} synth {synth}: {nenv} envs {time.time()-t0:.0f}s  fail {nfail}  oracle refused {nref}"
           f"  worst accepted err {worst:.1e}  steps mean {np.mean(steps):.2f} max {max(steps)}"
-          f"  rounds max {max(rounds)}")
+          f"  rounds max {max(rounds)}  eps {eps:.0e}  ipm it mean {np.mean(its):.2f}"
+          f" wave-max mean {np.mean(np.max(np.reshape(its, (-1, 4)), axis=1)):.2f} max {max(its)}"
+          f"  wave steps mean {np.mean(np.max(np.reshape(steps, (-1, 4)), axis=1)):.2f}"
+          f"  wave cost (it + 0.4 rounds + 0.15 steps) max "
+          f"{np.max(np.max(np.reshape(its, (-1, 4)), 1) + 0.4 * np.max(np.reshape(rounds, (-1, 4)), 1) + 0.15 * np.max(np.reshape(steps, (-1, 4)), 1)):.2f}"
+          f" p99 {np.percentile(np.max(np.reshape(its, (-1, 4)), 1) + 0.4 * np.max(np.reshape(rounds, (-1, 4)), 1) + 0.15 * np.max(np.reshape(steps, (-1, 4)), 1), 99):.2f}")
