@@ -655,12 +655,11 @@ def single_env(robot: str, ticks: int) -> dict:
 def ipm_kernel_name(robot: str, nenv: int, dev) -> str:
     """The interior-point kernel(s) one launch runs: past one resident wavefront per SIMD the
     cold WaLTER solve of at least four rounds of wavefronts runs the lockstep compaction's park and resume passes (csrc/osc_batch.hip,
-    ParkArgs; the default park iteration is 16 for WaLTER, off for Go2; OSC_PARK_IT overrides)."""
+    ParkArgs; the default park iteration, osc_model_tuning.park_it, is 16 for WaLTER, off for Go2)."""
     cus = (torch.cuda.get_device_properties(dev).multi_processor_count
            if torch.cuda.is_available() else 256)   # (CPU rehearsal of the rank path: MI355X)
     resident = 4 * 4 * cus
-    park = os.environ.get("OSC_PARK_IT", "16" if robot == "walter_sr" else "0")
-    if nenv >= 4 * resident and park not in ("", "0"):   # (kParkMinRounds)
+    if nenv >= 4 * resident and robot == "walter_sr":   # (kParkMinRounds)
         return "osc_ipm_compact_kernel (park + resume passes)"
     return "osc_ipm_kernel"
 

@@ -722,6 +722,9 @@ __device__ __forceinline__ void setup_env(
     i0 *= 2;
     j0 *= 2;
     double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
+#ifdef OSC_HA_UNROLL
+#pragma unroll OSC_HA_UNROLL
+#endif
     for (int r = 0; r < S; ++r) {
       const double2 x = *reinterpret_cast<const double2*>(sA + r * NAP + i0);
       const double2 y = *reinterpret_cast<const double2*>(sA + r * NAP + j0);
@@ -1253,40 +1256,53 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // (one ds_write instead of a lane select), each lane reads its own two back at the end.
 // Slot-1 lanes past N (N < 32) hold a copy of column N-1 (the caller loads jj1 = N-1 there);
 // they are left unmasked while column N-1 is still active, so they stay an exact mirror of it --
-// finite, and never a broadcast source.  (Issuing pivot k+1's broadcast and reciprocal inside
-// step k's trailing update measured ~1 % slower at Go2 4,096.)
+// finite, and never a broadcast source.
+// Look-ahead: pivot k+1's test, broadcast, reciprocal and scaling are issued right after step k's
+// first trailing FMA pair (which finalises column k+1's entry), so their dependent chain overlaps
+// the rest of step k's FMAs instead of stalling between the steps (bitwise the same factor;
+// profiles/r04f_ab_ldl_lookahead.jsonl: Go2 4,096 0.1737 -> 0.1721 ms per solve, 65,536 1.782 ->
+// 1.762, WaLTER 4,096 0.2804 -> 0.2758).
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
-  static_for<0, N>([&](auto kc) {
+  // pivot k's preparation: -> (t0, t1) = -L[lane][k] for the lanes still to be eliminated
+  auto prep = [&](auto kc, double& t0, double& t1) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    // Cholesky-infinity (Wright; PCx): a pivot not above 1e-13 x its column's original diagonal
-    // (thr, lane-local) becomes 1e128.  Every lane tests its own slot-s entry k; only the pivot
-    // lane's result -- the true diagonal -- is broadcast, so no LDS round trip per step.
     const double own = (s == 0) ? c0[k] : c1[k];
     const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
     const double inv = recip1(dk);
     sdinv[k] = inv;
-    // Row k of every column, scaled by -1/D_k once here, is all the triangular solves read of
-    // it: lanes j > k hold L[j][k] D_k -> -L[j][k] (forward), lanes j < k hold L[k][j] D_j ->
-    // -L[k][j] D_j / D_k (backward, D-scaled), so neither solve multiplies inside its chain.
     c0[k] = -c0[k] * inv;
     c1[k] = -c1[k] * inv;
-    // -L[lane][k] for the lanes still to be eliminated (slot 0: lane > k; slot 1: lane+16 > k,
-    // which holds for every slot-1 lane -- padding mirrors included -- while k < 16)
-    const double t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(c0[k]);
+    t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(c0[k]);
     constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
-    const double t1 = keep_lanes<rows_mask(kT1)>(c1[k]);
-    static_for<k + 1, N>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if constexpr (s == 0) {
-        fmac_bcast<kl>(c1[i], c0[i], t1);
-        if constexpr (k < kRow - 1) fmac_bcast_self<kl>(c0[i], t0);
-      } else {
-        fmac_bcast_self<kl>(c1[i], t1);
-      }
-    });
+    t1 = keep_lanes<rows_mask(kT1)>(c1[k]);
+  };
+  // one trailing FMA pair of step k, row i (NOP: the DPP source was written just before)
+  auto upd = [&](auto kc, auto ic, double t0, double t1) {
+    constexpr int k = decltype(kc)::value, i = decltype(ic)::value;
+    constexpr int s = k / kRow, kl = k % kRow;
+    constexpr bool nop = (i == k + 1) && (k >= 1) && (i == N - 1);
+    if constexpr (s == 0) {
+      fmac_bcast<kl, nop>(c1[i], c0[i], t1);
+      if constexpr (k < kRow - 1) fmac_bcast_self<kl>(c0[i], t0);
+    } else {
+      fmac_bcast_self<kl, nop>(c1[i], t1);
+    }
+  };
+  double ta0, ta1;
+  prep(std::integral_constant<int, 0>{}, ta0, ta1);
+  static_for<0, N>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    double tb0 = 0.0, tb1 = 0.0;
+    if constexpr (k + 1 < N) {
+      upd(kc, std::integral_constant<int, k + 1>{}, ta0, ta1);
+      prep(std::integral_constant<int, k + 1>{}, tb0, tb1);
+    }
+    static_for<k + 2, N>([&](auto ic) { upd(kc, ic, ta0, ta1); });
+    ta0 = tb0;
+    ta1 = tb1;
   });
   wave_sync();
   dinv0 = sdinv[l];
@@ -1991,7 +2007,7 @@ __device__ __forceinline__ void ipm_block(
     // `warm_restart`) is re-centred in place -- slacks h - G y + 1, multipliers 1: the cold
     // start's shape, no factorisation.  The rare solves that fall into a two-iteration limit
     // cycle of the step rule (mu oscillating near 1e-4; random-walk inputs, ~3e-6 of env-ticks,
-    // tools/warm_stalls.py) then finish ~10 iterations later instead of at max_iter.  No env of
+    // round-3 warm-stall study) then finish ~10 iterations later instead of at max_iter.  No env of
     // the fresh-batch sweeps is still that far off at iteration 20 (tools/ipm_model.py
     // "recenter20": identical iteration counts).
     bool restart = false;
@@ -2193,7 +2209,7 @@ __device__ __forceinline__ void ipm_block(
         if constexpr (WHR) {
           // late stall: once the active rows' barrier terms pass ~1e10 their dense rank-one terms
           // in the rotated Newton matrix swamp its small curvature and the affine step collapses
-          // (tools/wheel_one.py traces).  The iterate is as good as it gets there: stop on it
+          // (round-3 wheel traces).  The iterate is as good as it gets there: stop on it
           // (no step) and let the refinement finish the solve.
           if (!done && mu <= 1e-8 && step < 0.1 && rwmax <= P->wheel_tol) {
             done = true;
@@ -2303,11 +2319,24 @@ __device__ __forceinline__ void ipm_block(
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
       const double ytol = 1e-9 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)));
+      // (experiment switches for the wheel rows: OSC_WH_KKT -- the generic KKT acceptance and per-
+      // env convergence below instead of the fixed steps and move bound; OSC_WH_NOSTOL -- active
+      // set lambda > s only)
+#ifdef OSC_WH_KKT
+      constexpr bool kOldWh = false;
+#else
+      constexpr bool kOldWh = WHR;
+#endif
+#ifdef OSC_WH_NOSTOL
+      constexpr bool kWhStol = false;
+#else
+      constexpr bool kWhStol = true;
+#endif
       double Dr[NRL], mur[NRL];
       // WH: a row whose slack is within 1e-6 of the bound is active too -- next to the rows'
       // Schur solves the interior point's multipliers of a weakly active row can be off by orders
       // of magnitude while y is right (numpy model: 11 of 512 tumbling refinements rejected -> 0)
-      const double stol = D::WH ? 1e-6 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0))) : -1.0;
+      const double stol = (D::WH && kWhStol) ? 1e-6 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0))) : -1.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
         const bool a = act[t] && (lam[t] > s[t] || s[t] <= stol);
@@ -2458,7 +2487,7 @@ __device__ __forceinline__ void ipm_block(
         STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
         conv = false;
-        for (int k = 0; k < (WHR ? refine_steps : kRefineMaxSteps); ++k) {
+        for (int k = 0; k < (kOldWh ? refine_steps : (WHR ? 16 : kRefineMaxSteps)); ++k) {
           // WH: X holds X^ = X'T, so dv = X^ [y^; 1] (y^ = T'y staged in sVy2, free until the step)
           // and the rows' residual at y comes with y^
           const double* yv = sVy;
@@ -2582,7 +2611,7 @@ __device__ __forceinline__ void ipm_block(
             rot_out(d0, d1, d0, d1);
             dlast = row_max(fmax(fabs(d0), v1 ? fabs(d1) : 0.0));
           }
-          const bool frz = !WHR && conv;   // converged at an earlier step: no further move
+          const bool frz = !kOldWh && conv;   // converged at an earlier step: no further move
           if (frz) {
             d0 = 0.0;
             d1 = 0.0;
@@ -2598,7 +2627,7 @@ __device__ __forceinline__ void ipm_block(
           sVy[j0] = ya0;
           if (v1) sVy[j1] = ya1;
           wave_sync();
-          if constexpr (!WHR) {
+          if constexpr (!kOldWh) {
             // converged: the step fell below 1e-10 of the env's |y| (a row-wide scale: a lane
             // holding only near-zero variables must not hold the env to 1e-10 absolute)
             const double dn = row_max(fmax(fabs(d0), v1 ? fabs(d1) : 0.0));
@@ -2638,7 +2667,7 @@ __device__ __forceinline__ void ipm_block(
         // a round whose steps have not converged asks for another one as well (it restarts
         // from the interior point's iterate with the multipliers carried over)
         const bool more =
-            viol_env || (mine && (WHR ? dlast > 1e-10 * (1.0 + yscale) : !conv));
+            viol_env || (mine && (kOldWh ? dlast > 1e-10 * (1.0 + yscale) : !conv));
         // an env whose round ended without a violation is final: a further round that a wave-mate
         // asks for must not move it (its multipliers carry over between rounds), so each env's
         // result is independent of the envs sharing its wavefront -- and of the compaction's
@@ -2675,7 +2704,7 @@ __device__ __forceinline__ void ipm_block(
       // env's |y| scale, a row-wide maximum -- within 0.1 of y)
       const double ok =
           (isfinite(ya0) && isfinite(ya1) &&
-           (WHR ? (mv <= 0.1 * (1.0 + myr) && dlast <= 1e-10 * (1.0 + myr))
+           (kOldWh ? (mv <= 0.1 * (1.0 + myr) && dlast <= 1e-10 * (1.0 + myr))
                 : (settled && mv <= P->refine_max_move * (1.0 + myr)))) ? 1.0 : 0.0;
       // (WH: and the wheel rows hold at the refined point)
       double wres = 0.0;
@@ -3289,7 +3318,7 @@ extern "C" int osc_model_create_tuned(const osc_model_desc* desc, const osc_mode
   // One-wave-per-SIMD variant up to the batch that fills every SIMD once; beyond it the
   // two-waves variant, except for the 32-column WaLTER system, whose Newton matrix does not fit
   // two waves' register budget (scratch spills): it always runs one wave per SIMD with AGPR
-  // spill space (MI355X, 32,768 envs: 2.61 vs 2.95 ms; tools/variant_sweep.sh).
+  // spill space (MI355X, 32,768 envs: 2.61 vs 2.95 ms; round-2 variant sweep).
   m->small_batch_max = (kid == K_GO2) ? kEnvPerWave * 4 * cus : INT32_MAX;
   if (t.small_batch_max >= 0) m->small_batch_max = t.small_batch_max;
   if (kid == K_WALTER_WHEELS) m->small_batch_max = INT32_MAX;   // (one-wave kernel only)

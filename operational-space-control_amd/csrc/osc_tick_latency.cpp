@@ -25,7 +25,8 @@
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    std::fprintf(stderr, "usage: osc_tick_latency <robot> <tree path or \"\"> <ticks> [warmup]\n");
+    std::fprintf(stderr, "usage: osc_tick_latency <robot> <tree path or \"\"> <ticks> [warmup]"
+                         " [warm_delta warm_center]\n");
     return 2;
   }
   const std::string robot = argv[1];
@@ -35,6 +36,8 @@ int main(int argc, char** argv) {
   if (osc_desc_from_yaml(robot.c_str(), nullptr, &d) != OSC_OK) return 3;
 
   osc_amd::OperationalSpaceController c(robot, "", 2000, argv[2]);
+  // optional 5th / 6th arguments: the warm start's floors (A/B of set_warm_start_floors)
+  if (argc > 6) c.set_warm_start_floors(std::atof(argv[5]), std::atof(argv[6]));
   osc_amd::State s;
   s.motor_position.assign(d.nu, 0.0);
   s.motor_velocity.assign(d.nu, 0.0);

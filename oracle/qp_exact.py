@@ -319,21 +319,41 @@ def _dual_active_set(qp: QPData, eq, ineq, max_iter: int = 5000):
     return [k - neq for k in act if k >= neq], it
 
 
-def _finish(model: OSCModel, qp: QPData, eq, ineq, W, it, refine_steps: int) -> ExactSolution:
+def _finish(model: OSCModel, qp: QPData, eq, ineq, W, it, refine_steps: int,
+            basis: bool = False) -> ExactSolution:
     """Exact KKT solve on the identified working set W, polished by mixed-precision iterative
-    refinement, with the multipliers mapped to OSQP's convention and the KKT certificate."""
+    refinement, with the multipliers mapped to OSQP's convention and the KKT certificate.
+    basis=True (the retry when the first solve ends off the equality rows): the working set's rows
+    are first reduced to a basis of their span by QR with column pivoting -- a nearly dependent
+    working set (wheel rows next to an apex contact) makes the full KKT matrix numerically
+    singular, while the optimum (unique, H > 0) satisfies every row of the span; the dropped rows
+    get zero multipliers."""
     n = model.n
     A = qp.A
     Aeq = A[eq]
     neq = Aeq.shape[0]
     rows = np.vstack([Aeq] + [ineq[w][1] * A[ineq[w][0]][None, :] for w in W])
     rhs_b = np.concatenate([qp.u[eq]] + [[ineq[w][2]] for w in W]) if W else qp.u[eq]
+    keep = np.arange(rows.shape[0])
+    if basis and rows.shape[0]:
+        import scipy.linalg
+        un = rows / np.linalg.norm(rows, axis=1, keepdims=True)
+        _, R, piv = scipy.linalg.qr(un.T, mode="economic", pivoting=True)
+        d = np.abs(np.diag(R))
+        keep = np.sort(piv[:int((d > 1e-9 * d[0]).sum())])
+        rows, rhs_b = rows[keep], rhs_b[keep]
     k = rows.shape[0]
     K = np.zeros((n + k, n + k))
     K[:n, :n] = qp.H
     K[:n, n:] = rows.T
     K[n:, :n] = rows
     rhs = np.concatenate([-qp.f, rhs_b])
+    if basis:   # (the retry: the whole solve in extended precision, then refined there)
+        Kl = K.astype(np.longdouble)
+        soll = _solve_ld(Kl, rhs)
+        for _ in range(refine_steps):
+            soll = soll + _solve_ld(Kl, rhs.astype(np.longdouble) - Kl @ soll)
+        return _finish_tail(model, qp, eq, ineq, W, it, soll.astype(np.float64), keep, basis)
     sol = _kkt_solve(K, rhs)
     # Mixed-precision iterative refinement: residuals in x87 extended precision (eps ~1e-19),
     # corrections from the fp64 factorisation.  Converges to ~eps_ext * cond(K), i.e. well
@@ -344,12 +364,22 @@ def _finish(model: OSCModel, qp: QPData, eq, ineq, W, it, refine_steps: int) -> 
     for _ in range(refine_steps):
         r = rhsl - Kl @ soll
         soll = soll + _kkt_solve(K, r.astype(np.float64)).astype(np.longdouble)
-    sol = soll.astype(np.float64)
-    x, lam = sol[:n], sol[n:]
-    # a degenerate working set whose KKT system came back inconsistent (the active-set method does
-    # not resolve every such case): refuse rather than return a point off the equality rows
+    return _finish_tail(model, qp, eq, ineq, W, it, soll.astype(np.float64), keep, basis)
+
+
+def _finish_tail(model, qp, eq, ineq, W, it, sol, keep, basis):
+    n = model.n
+    A = qp.A
+    neq = len(eq)
+    x, lam_k = sol[:n], sol[n:]
+    lam = np.zeros(neq + len(W))
+    lam[keep] = lam_k
+    # a degenerate working set whose KKT system came back inconsistent: once more on a basis of
+    # its rows, then refuse rather than return a point off the equality rows
     eq_res = np.abs(A[eq] @ x - qp.u[eq]).max() if eq else 0.0
     if not eq_res <= 1e-8 * (1.0 + np.abs(qp.u[eq]).max() if eq else 1.0):
+        if not basis:
+            return _finish(model, qp, eq, ineq, W, it, 4, basis=True)
         raise RuntimeError(f"active set ended off the equality rows ({eq_res:.1e})")
     y = np.zeros(A.shape[0])
     y[eq] += lam[:neq]
@@ -363,6 +393,29 @@ def _finish(model: OSCModel, qp: QPData, eq, ineq, W, it, refine_steps: int) -> 
     return ExactSolution(x=x, y=y, active=active, iterations=it, cert=cert)
 
 
+def _solve_ld(K, rhs):
+    """Gaussian elimination with partial pivoting in x87 extended precision (eps ~1e-19), for the
+    final KKT system of a working set that is nearly dependent (wheel rows whose smallest singular
+    value is ~1e-8 of the largest: its fp64 factorisation cannot serve iterative refinement)."""
+    A = np.array(K, dtype=np.longdouble)
+    b = np.array(rhs, dtype=np.longdouble)
+    n = A.shape[0]
+    for k in range(n):
+        p = k + int(np.argmax(np.abs(A[k:, k])))
+        if p != k:
+            A[[k, p]] = A[[p, k]]
+            b[[k, p]] = b[[p, k]]
+        if A[k, k] == 0:
+            continue
+        f = A[k + 1:, k] / A[k, k]
+        A[k + 1:, k:] -= f[:, None] * A[k, k:][None, :]
+        b[k + 1:] -= f * b[k]
+    x = np.zeros(n, dtype=np.longdouble)
+    for k in range(n - 1, -1, -1):
+        x[k] = (b[k] - A[k, k + 1:] @ x[k + 1:]) / A[k, k] if A[k, k] != 0 else 0
+    return x
+
+
 def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
                 refine_steps: int = 4, method: str = "auto") -> ExactSolution:
     """The QP's unique optimum with its KKT certificate.  method "primal": the primal active-set
@@ -372,7 +425,10 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
     if method in ("primal", "auto"):
         try:
             W, it = _primal_active_set(model, qp, M, C, J, eq, ineq, max_iter)
-            return _finish(model, qp, eq, ineq, W, it, refine_steps)
+            sol = _finish(model, qp, eq, ineq, W, it, refine_steps)
+            # (auto: a primal working set whose certificate fails goes to the dual method too)
+            if method == "primal" or certified(sol.cert, 1e-8):
+                return sol
         except RuntimeError:
             if method == "primal":
                 raise
