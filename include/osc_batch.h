@@ -221,9 +221,9 @@ int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double
  * it has no inequality rows.  Each call reads the state and writes this tick's solution back.
  * Results agree with the cold solve to the solve's tolerance; the iteration count drops when
  * consecutive ticks are close.  A warm env that stalls is re-centred in place,
- * and any env the warm pass leaves unconverged (OSC_SOLVE_MAX_ITER / _NUMERICAL) is re-solved
- * cold by a second launch that only the wavefronts holding such an env execute (an
- * OSC_SOLVE_UNREFINED env is not: the cold solve rejects the same refinement). */
+ * and any env the warm pass leaves not OK (OSC_SOLVE_MAX_ITER / _NUMERICAL / _UNREFINED) is
+ * re-solved cold, to mu <= 1e-12, by a second launch that only the wavefronts holding such an env
+ * execute. */
 int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
 int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
                          const double* M, const double* C, const double* J, const double* b,

@@ -130,7 +130,7 @@ class OperationalSpaceController {
    * initialize_thread. */
   void set_tick_graph(bool on) { use_graph_ = on; }
   /* The warm start's floors for the controller's one-env ticks (osc_model_tuning warm_delta /
-   * warm_center; default 0.1 / 0.3).  Call before initialize_optimization. */
+   * warm_center; default 0.3 / 0.3).  Call before initialize_optimization. */
   void set_warm_start_floors(double delta, double center) {
     single_env_warm_delta_ = delta;
     single_env_warm_center_ = center;
@@ -186,7 +186,7 @@ class OperationalSpaceController {
   int graph_kind_ = -1;
   size_t graph_in_bytes_ = 0;
   bool use_graph_ = false;          // set_tick_graph: replay the tick as a hipGraph
-  double single_env_warm_delta_ = 0.1;    // set_warm_start_floors
+  double single_env_warm_delta_ = 0.3;    // set_warm_start_floors
   double single_env_warm_center_ = 0.3;
 };
 

@@ -2721,8 +2721,13 @@ __device__ __forceinline__ void ipm_block(
         st = OSC_SOLVE_OK;
       }
       // a converged env whose refinement is rejected keeps the interior point's iterate, and says
-      // so: it is only as accurate as the interior point's stop
-      if (mine && !keep && st == OSC_SOLVE_OK) st = OSC_SOLVE_UNREFINED;
+      // so: it is only as accurate as the interior point's stop.  (Wheel rows: the interior point
+      // runs to mu <= 1e-12 and its pinned coordinates hold the rows to rounding; where they hold
+      // to ytol its iterate stands as the solution -- census, profiles/r04g_census_*: every such
+      // env within 4e-12 of the exact optimum, while the refinement, started from it, ended with
+      // rows violated after its rounds; the exported duals come from stationarity, not from the
+      // refinement, osc_dual_kernel)
+      if (mine && !keep && st == OSC_SOLVE_OK && !(WHR && rwmax <= ytol)) st = OSC_SOLVE_UNREFINED;
 #ifdef OSC_REFINE_DIAG   // diagnostic builds only: why the refinement was rejected
       if (mine && !keep)
         st = OSC_SOLVE_UNREFINED + 16 * (viol_env ? 1 : 0) + 32 * (row_min(ok) == 1.0 ? 0 : 1) +
@@ -2910,20 +2915,187 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     sg[lane] = a;
   }
   __syncthreads();
-  if constexpr (D::WH) {
-    // nu_w = R'(w - V g0): the interior point's rows were Q = L V X with V = R E (setup_env);
-    // stationarity X'(g0 + E'nu_w) = X'(g0 - V'V g0) + Q'nu_Q holds with E'nu_w = V'(L'nu_Q - V g0)
-    __shared__ double st[NW > 0 ? NW : 1];
-    if (lane < NW) {
-      double a = w[D::W_NU + lane];
-      for (int j = 0; j < NV; ++j) a = fma(-w[D::W_WV + lane * NV + j], sg[j], a);
-      st[lane] = a;
+  for (int k = 0; k < NV; ++k) {   // M = L L' (lower triangle of sL), column k
+    double t = 0.0;
+    if (lane >= k && lane < NV) {
+      t = sL[lane * NV + k];
+      for (int p = 0; p < k; ++p) t = fma(-sL[lane * NV + p], sL[k * NV + p], t);
+      sL[lane * NV + k] = t;
     }
     __syncthreads();
+    const double dk = sqrt(sL[k * NV + k]);
+    __syncthreads();
+    if (lane >= k && lane < NV) sL[lane * NV + k] = (lane == k) ? dk : t / dk;
+    __syncthreads();
+  }
+  // L L' v = b in place (one lane, serial)
+  auto chol_solve = [&](double* v) {
+    for (int i = 0; i < NV; ++i) {
+      double a = v[i];
+      for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], v[p], a);
+      v[i] = a / sL[i * NV + i];
+    }
+    for (int i = NV - 1; i >= 0; --i) {
+      double a = v[i];
+      for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], v[p], a);
+      v[i] = a / sL[i * NV + i];
+    }
+  };
+  if constexpr (D::WH) {
+    // The wheel rows' multipliers nu_w from stationarity itself (round 4; was: the refinement's
+    // last residual, W_NU, which exists only where the refinement was kept and is not unique
+    // where the rows are dependent).  With E the rows (mask-scaled), W = M^-1 E' and
+    // nu0 = -M^-1 g0, the dynamics multipliers are nu = nu0 - W nu_w, and nu_w must make
+    //   every torque off its bounds:   nu[NB + q] = 2 (w_tau + w_reg) u_q       (its box y = 0)
+    //   every contact in touch:        r_k = 2 w_reg z_k - Jc_k' nu  in the span of its active
+    //                                  rows' normals (component orthogonal to them = 0)
+    // -- a small linear least-squares problem in nu_w (<= nu + 3 nc rows, 2 nc unknowns),
+    // solved for its minimum-norm solution (Tikhonov 1e-13 x trace: dependent rows get the
+    // smallest multipliers).  The contact multipliers then follow by the NNLS below.
+    __shared__ double sE[NW > 0 ? NW * NV : 1];      // E, then W' (row w = column w of W)
+    __shared__ double sv0[NV];                       // nu0
+    __shared__ double sA[(NU + 3 * NC) * (NW > 0 ? NW : 1)];
+    __shared__ double sb[NU + 3 * NC];
+    __shared__ int snrow;
+    __shared__ double sN[NW > 0 ? NW : 1][NW > 0 ? NW : 1];
+    __shared__ double sr2[NW > 0 ? NW : 1];
+    const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
     if (lane < NW) {
-      double a = 0.0;
-      for (int v = 0; v < NW; ++v) a = fma(w[D::W_WR + v * NW + lane], st[v], a);
-      snu[lane] = a;
+      const int i = lane / 2, side = lane % 2;
+      for (int j = 0; j < NV; ++j) {
+        double e = 0.0;
+        for (int c = 0; c < 3; ++c) e = fma(wd[6 * i + 3 * side + c], J[(JC0 + 3 * i + c) * NV + j], e);
+        if (side == 0 && j == P->wheel_dof[i]) e -= P->wheel_radius[i];
+        sE[lane * NV + j] = mask[i] * e;
+      }
+    }
+    if (lane < NV) sv0[lane] = -sg[lane];
+    __syncthreads();
+    if (lane < NW) chol_solve(sE + lane * NV);        // row w <- (M^-1 E')[:, w]
+    if (lane == NW) chol_solve(sv0);                  // nu0 = -M^-1 g0
+    __syncthreads();
+    if (lane == 0) {
+      const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg, mu = P->mu;
+      int n = 0;
+      for (int q = 0; q < NU; ++q) {   // torques off their bounds
+        const double u = x[NV + q];
+        const double tol = 1e-9 * (1.0 + fabs(u));
+        const bool hi = fabs(P->u_ub[q]) < P->inf_thresh && u >= P->u_ub[q] - tol;
+        const bool lo = fabs(P->u_lb[q]) < P->inf_thresh && u <= P->u_lb[q] + tol;
+        if (hi || lo) continue;
+        for (int w = 0; w < NW; ++w) sA[n * NW + w] = -sE[w * NV + NB + q];
+        sb[n++] = wu * u - sv0[NB + q];
+      }
+      for (int k = 0; k < NC; ++k) {   // contacts in touch: r_k orthogonal to no active normal
+        if (mask[k] == 0.0) continue;
+        const double f0 = x[NV + NU + 3 * k], f1 = x[NV + NU + 3 * k + 1], f2 = x[NV + NU + 3 * k + 2];
+        const double tol = 1e-9 * (1.0 + fmax(fabs(f0), fmax(fabs(f1), fabs(f2))));
+        double q[3][3];   // orthonormal basis of the active normals' span (Gram-Schmidt)
+        int rk = 0;
+        const double ub = P->z_ub[2] * mask[k], lb = P->z_lb[2] * mask[k];
+        for (int i = 0; i < 6; ++i) {
+          double g[3];
+          double gap;
+          if (i < 4) {
+            g[0] = (i & 1) ? -1.0 : 1.0; g[1] = (i >= 2) ? -1.0 : 1.0; g[2] = -mu;
+            gap = -(g[0] * f0 + g[1] * f1 + g[2] * f2);
+          } else if (i == 4) {
+            if (!(fabs(lb) < P->inf_thresh)) continue;
+            g[0] = g[1] = 0.0; g[2] = -1.0; gap = f2 - lb;
+          } else {
+            if (!(fabs(ub) < P->inf_thresh)) continue;
+            g[0] = g[1] = 0.0; g[2] = 1.0; gap = ub - f2;
+          }
+          if (gap > tol || rk == 3) continue;
+          for (int a = 0; a < rk; ++a) {
+            const double d = g[0] * q[a][0] + g[1] * q[a][1] + g[2] * q[a][2];
+            for (int c = 0; c < 3; ++c) g[c] -= d * q[a][c];
+          }
+          const double nn = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+          if (nn > 1e-6) {
+            for (int c = 0; c < 3; ++c) q[rk][c] = g[c] / nn;
+            ++rk;
+          }
+        }
+        // complement: e_c orthogonalised against the span and the complement vectors so far
+        int nc = 0;
+        double pc[3][3];
+        for (int c = 0; c < 3 && rk + nc < 3; ++c) {
+          double v[3] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0};
+          for (int a = 0; a < rk; ++a) {
+            const double d = v[0] * q[a][0] + v[1] * q[a][1] + v[2] * q[a][2];
+            for (int e = 0; e < 3; ++e) v[e] -= d * q[a][e];
+          }
+          for (int a = 0; a < nc; ++a) {
+            const double d = v[0] * pc[a][0] + v[1] * pc[a][1] + v[2] * pc[a][2];
+            for (int e = 0; e < 3; ++e) v[e] -= d * pc[a][e];
+          }
+          const double nn = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+          if (nn < 0.5) continue;
+          for (int e = 0; e < 3; ++e) pc[nc][e] = v[e] / nn;
+          // p' r_k = 0 with r_k = wz f - Jc_k' (nu0 - W nu_w)
+          double rhs = 0.0;
+          double* row = sA + n * NW;   // (built in place)
+          for (int w = 0; w < NW; ++w) row[w] = 0.0;
+          for (int cc = 0; cc < 3; ++cc) {
+            const double* jr = J + (JC0 + 3 * k + cc) * NV;
+            double jn0 = 0.0;
+            for (int i = 0; i < NV; ++i) jn0 = fma(jr[i], sv0[i], jn0);
+            const double fc = cc == 0 ? f0 : (cc == 1 ? f1 : f2);
+            rhs = fma(pc[nc][cc], wz * fc - jn0, rhs);
+            for (int w = 0; w < NW; ++w) {
+              double jw = 0.0;
+              for (int i = 0; i < NV; ++i) jw = fma(jr[i], sE[w * NV + i], jw);
+              row[w] = fma(pc[nc][cc], jw, row[w]);
+            }
+          }
+          sb[n++] = -rhs;   // row . nu_w = -rhs
+          ++nc;
+        }
+      }
+      snrow = n;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      // minimum-norm least squares: (A'A + d I) nu_w = A'b, Cholesky in place (NW <= 16)
+      const int n = snrow;
+      double (*N)[NW > 0 ? NW : 1] = sN;   // (LDS: no per-lane scratch)
+      double* r = sr2;
+      double tr = 0.0;
+      for (int a = 0; a < NW; ++a) {
+        double rb = 0.0;
+        for (int t = 0; t < n; ++t) rb = fma(sA[t * NW + a], sb[t], rb);
+        r[a] = rb;
+        for (int c = 0; c <= a; ++c) {
+          double v = 0.0;
+          for (int t = 0; t < n; ++t) v = fma(sA[t * NW + a], sA[t * NW + c], v);
+          N[a][c] = v;
+        }
+        tr += N[a][a];
+      }
+      const double dreg = 1e-13 * fmax(tr, 1e-300);
+      for (int a = 0; a < NW; ++a) N[a][a] += dreg;
+      for (int a = 0; a < NW; ++a) {
+        for (int c = 0; c < a; ++c) {
+          double v = N[a][c];
+          for (int e = 0; e < c; ++e) v -= N[a][e] * N[c][e];
+          N[a][c] = v / N[c][c];
+        }
+        double v = N[a][a];
+        for (int e = 0; e < a; ++e) v -= N[a][e] * N[a][e];
+        N[a][a] = sqrt(fmax(v, dreg));
+      }
+      for (int a = 0; a < NW; ++a) {
+        double v = r[a];
+        for (int e = 0; e < a; ++e) v -= N[a][e] * r[e];
+        r[a] = v / N[a][a];
+      }
+      for (int a = NW - 1; a >= 0; --a) {
+        double v = r[a];
+        for (int e = a + 1; e < NW; ++e) v -= N[e][a] * r[e];
+        r[a] = v / N[a][a];
+      }
+      for (int a = 0; a < NW; ++a) snu[a] = r[a];
     }
   }
   __syncthreads();
@@ -2946,19 +3118,6 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     sg[lane] = -a;
   }
   __syncthreads();
-  for (int k = 0; k < NV; ++k) {   // M = L L' (lower triangle of sL), column k
-    double t = 0.0;
-    if (lane >= k && lane < NV) {
-      t = sL[lane * NV + k];
-      for (int p = 0; p < k; ++p) t = fma(-sL[lane * NV + p], sL[k * NV + p], t);
-      sL[lane * NV + k] = t;
-    }
-    __syncthreads();
-    const double dk = sqrt(sL[k * NV + k]);
-    __syncthreads();
-    if (lane >= k && lane < NV) sL[lane * NV + k] = (lane == k) ? dk : t / dk;
-    __syncthreads();
-  }
   if (lane == 0) {   // L L' nu = -g_x
     for (int i = 0; i < NV; ++i) {
       double a = sg[i];

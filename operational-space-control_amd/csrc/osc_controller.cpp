@@ -100,10 +100,10 @@ Status OperationalSpaceController::initialize(State initial_state) {
 Status OperationalSpaceController::initialize_optimization() {
   if (!initialized_) return FailedPreconditionError("Operational Space Controller not initialized.");
   if (optimization_initialized_) return Status::Ok();
-  // One env per tick: the warm start's tighter floors of round 2 (delta 0.1, centring 0.3) --
-  // the batch defaults (1, 1) cut the slowest warm envs' tail of a 4,096-env wave set, which a lone
-  // env does not have, and cost it +0.8 mean iterations (single-env tick median 92 -> 99 us,
-  // DESIGN.md §10)
+  // One env per tick: tighter warm-start floors than the batch defaults (1, 1), which cut the
+  // slowest warm envs' tail of a 4,096-env wave set -- a tail a lone env does not have -- at +0.8
+  // mean iterations.  Measured over 2,000 Go2 ticks (profiles/r04g_tick_*.json, median / p99 us):
+  // (1, 1) 93.1 / 117.6, (0.1, 0.3) 85.0 / 133.1, (0.3, 0.3) 90.6 / 122.0
   osc_model_tuning tune;
   Status st = from_osc(osc_model_tuning_defaults(&desc_, &tune), "osc_model_tuning_defaults");
   if (!st.ok()) return st;

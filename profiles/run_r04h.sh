@@ -6,6 +6,8 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 export TMPDIR=/tmp
 B="--no-cpu --no-warm --no-front-end --no-single-env --no-north-star --no-mixed"
+mkdir -p gpurun_out/r04h
+timeout -k 10 90 rocprofv3 -L > gpurun_out/r04h/counters_list.txt 2>&1 || exit 20
 for n in 4096 8192 65536; do
   O=gpurun_out/r04h/$n
   mkdir -p $O

@@ -286,15 +286,12 @@ def test_wheel_rows_kkt_certificate(gpu):
     assert (st == 0).mean() >= 0.98, (np.bincount(st), np.nonzero(st)[0][:20])
     cert = _kkt(*_batched_qp("walter_sr_wheels", *args, wheel, wdt), out.x, out.y)
     ok = torch.from_numpy(st == 0).cuda()
-    # known gap: the rows' multipliers come from the refinement's last residual, and
-    # on a few envs whose active set changed in its last rounds they are not yet converged -- so
-    # the certificate is required of 98 % of the envs reported OK, not all
-    good = torch.ones_like(ok)
+    # every env reported OK is certified (the rows' multipliers from stationarity itself,
+    # osc_dual_kernel, round 4: was 98 % with them from the refinement's last residual)
     for k, tol in (("stationarity", KKT_STAT), ("primal", KKT_PRIMAL), ("dual", KKT_DUAL),
                    ("complementarity", KKT_COMP)):
-        good &= cert[k] <= tol
-    frac = (good & ok).sum().item() / max(ok.sum().item(), 1)
-    assert frac >= 0.98, (frac, {k: v[ok].max().item() for k, v in cert.items()})
+        v = cert[k][ok]
+        assert v.max().item() <= tol, (k, v.max().item(), int(torch.nonzero(ok)[v.argmax()].item()))
 
 
 def test_rejected_refinement_is_reported(gpu):

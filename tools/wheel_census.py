@@ -72,7 +72,7 @@ def main():
             err = float(np.abs(tau[e] - ref).max() / max(np.abs(ref).max(), 1.0))
             print(json.dumps({"tick": tick, "env": int(e), "status": int(st[e]), "iters": int(it[e]),
                               "certified": bool(good[e]), "err": err,
-                              "stationarity": float(cert["stationarity"][e].item()),
+                              "cert": {k: float(v[e].item()) for k, v in cert.items()},
                               "ncontact": int(d["mask"][e].sum())}), flush=True)
         d = random_walk(d, rng)
 
