@@ -1262,6 +1262,10 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // the rest of step k's FMAs instead of stalling between the steps (bitwise the same factor;
 // profiles/r04f_ab_ldl_lookahead.jsonl: Go2 4,096 0.1737 -> 0.1721 ms per solve, 65,536 1.782 ->
 // 1.762, WaLTER 4,096 0.2804 -> 0.2758).
+// (Fusing pass 0's forward elimination into the factorisation -- the right-hand side formed
+// first, its step k riding along the factor's -- measured within noise: Go2 4,096 0.1739 vs
+// 0.1718 ms per solve, 65,536 1.760 vs 1.748, WaLTER 4,096 0.2754 vs 0.2768, and not bitwise;
+// profiles/r04k/ab_fwd_fused.jsonl.)
 template <int N>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
@@ -2309,6 +2313,7 @@ __device__ __forceinline__ void ipm_block(
   // discarded.
   // (wheel rows: a fixed step count, the same whether or not the duals are asked for, so x and tau
   // do not depend on want_dual -- the rows' multipliers converge more slowly than y, hence 12)
+  if constexpr (CP == kCpPark) write_out = write_out && !parked;   // the resume pass writes them
   const int refine_steps = P->refine_steps;
   if constexpr (RF != kRfNone) {
     // WH: an env the interior point left at max_iter is refined too (its rotated Newton systems
@@ -2319,24 +2324,15 @@ __device__ __forceinline__ void ipm_block(
     if (P->refine_steps > 0 && __ballot(mine) != 0) {
       const double dpen = P->refine_penalty * row_max(fmax(fabs(hdg0), fabs(hdg1)));
       const double ytol = 1e-9 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0)));
-      // (experiment switches for the wheel rows: OSC_WH_KKT -- the generic KKT acceptance and per-
-      // env convergence below instead of the fixed steps and move bound; OSC_WH_NOSTOL -- active
-      // set lambda > s only)
-#ifdef OSC_WH_KKT
-      constexpr bool kOldWh = false;
-#else
+      // the wheel rows keep round 3's fixed steps and move-bound acceptance (their refinement runs
+      // refine_steps steps; the generic KKT acceptance measured no different on them)
       constexpr bool kOldWh = WHR;
-#endif
-#ifdef OSC_WH_NOSTOL
-      constexpr bool kWhStol = false;
-#else
-      constexpr bool kWhStol = true;
-#endif
       double Dr[NRL], mur[NRL];
       // WH: a row whose slack is within 1e-6 of the bound is active too -- next to the rows'
       // Schur solves the interior point's multipliers of a weakly active row can be off by orders
       // of magnitude while y is right (numpy model: 11 of 512 tumbling refinements rejected -> 0)
-      const double stol = (D::WH && kWhStol) ? 1e-6 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0))) : -1.0;
+      const double stol =
+          D::WH ? 1e-6 * (1.0 + row_max(fmax(fabs(y0), v1 ? fabs(y1) : 0.0))) : -1.0;
 #pragma unroll
       for (int t = 0; t < NRL; ++t) {
         const bool a = act[t] && (lam[t] > s[t] || s[t] <= stol);
@@ -2487,7 +2483,7 @@ __device__ __forceinline__ void ipm_block(
         STAMP_END(8);   // (the loop's slot 8 doubles as the refinement's LDL)
         STAMP_BEGIN();
         conv = false;
-        for (int k = 0; k < (kOldWh ? refine_steps : (WHR ? 16 : kRefineMaxSteps)); ++k) {
+        for (int k = 0; k < (kOldWh ? refine_steps : kRefineMaxSteps); ++k) {
           // WH: X holds X^ = X'T, so dv = X^ [y^; 1] (y^ = T'y staged in sVy2, free until the step)
           // and the rows' residual at y comes with y^
           const double* yv = sVy;
@@ -2949,16 +2945,14 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     //   every torque off its bounds:   nu[NB + q] = 2 (w_tau + w_reg) u_q       (its box y = 0)
     //   every contact in touch:        r_k = 2 w_reg z_k - Jc_k' nu  in the span of its active
     //                                  rows' normals (component orthogonal to them = 0)
-    // -- a small linear least-squares problem in nu_w (<= nu + 3 nc rows, 2 nc unknowns),
-    // solved for its minimum-norm solution (Tikhonov 1e-13 x trace: dependent rows get the
-    // smallest multipliers).  The contact multipliers then follow by the NNLS below.
+    // -- a small linear least-squares problem in nu_w (<= nu + 3 nc rows, 2 nc unknowns).  The
+    // contact multipliers then follow by the NNLS below.
     __shared__ double sE[NW > 0 ? NW * NV : 1];      // E, then W' (row w = column w of W)
     __shared__ double sv0[NV];                       // nu0
     __shared__ double sA[(NU + 3 * NC) * (NW > 0 ? NW : 1)];
     __shared__ double sb[NU + 3 * NC];
     __shared__ int snrow;
-    __shared__ double sN[NW > 0 ? NW : 1][NW > 0 ? NW : 1];
-    __shared__ double sr2[NW > 0 ? NW : 1];
+    __shared__ int spiv[NW > 0 ? NW : 1];
     const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
     if (lane < NW) {
       const int i = lane / 2, side = lane % 2;
@@ -3057,45 +3051,63 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     }
     __syncthreads();
     if (lane == 0) {
-      // minimum-norm least squares: (A'A + d I) nu_w = A'b, Cholesky in place (NW <= 16)
+      // the basic least-squares solution by Householder QR with column pivoting (rank: |R_jj| >
+      // 1e-10 |R_00|; the dependent rows' multipliers are zero).  (Normal equations do not do:
+      // the rows that fix dv need multipliers up to ~1e6 along directions whose singular values
+      // are ~1e-9 of the largest -- squared, they drown in rounding.)
       const int n = snrow;
-      double (*N)[NW > 0 ? NW : 1] = sN;   // (LDS: no per-lane scratch)
-      double* r = sr2;
-      double tr = 0.0;
-      for (int a = 0; a < NW; ++a) {
-        double rb = 0.0;
-        for (int t = 0; t < n; ++t) rb = fma(sA[t * NW + a], sb[t], rb);
-        r[a] = rb;
-        for (int c = 0; c <= a; ++c) {
+      double* A = sA;
+      double* bb = sb;
+      for (int c = 0; c < NW; ++c) spiv[c] = c;
+      double nmax0 = 0.0;
+      int rank = 0;
+      for (int j = 0; j < NW && j < n; ++j) {
+        int p = j;
+        double best = -1.0;
+        for (int c = j; c < NW; ++c) {
           double v = 0.0;
-          for (int t = 0; t < n; ++t) v = fma(sA[t * NW + a], sA[t * NW + c], v);
-          N[a][c] = v;
+          for (int t = j; t < n; ++t) v = fma(A[t * NW + c], A[t * NW + c], v);
+          if (v > best) { best = v; p = c; }
         }
-        tr += N[a][a];
-      }
-      const double dreg = 1e-13 * fmax(tr, 1e-300);
-      for (int a = 0; a < NW; ++a) N[a][a] += dreg;
-      for (int a = 0; a < NW; ++a) {
-        for (int c = 0; c < a; ++c) {
-          double v = N[a][c];
-          for (int e = 0; e < c; ++e) v -= N[a][e] * N[c][e];
-          N[a][c] = v / N[c][c];
+        const double cn = sqrt(best);
+        if (j == 0) nmax0 = cn;
+        if (!(cn > 1e-10 * nmax0) || cn == 0.0) break;
+        if (p != j) {
+          for (int t = 0; t < n; ++t) {
+            const double tmp = A[t * NW + j];
+            A[t * NW + j] = A[t * NW + p];
+            A[t * NW + p] = tmp;
+          }
+          const int ti = spiv[j]; spiv[j] = spiv[p]; spiv[p] = ti;
         }
-        double v = N[a][a];
-        for (int e = 0; e < a; ++e) v -= N[a][e] * N[a][e];
-        N[a][a] = sqrt(fmax(v, dreg));
+        const double ajj = A[j * NW + j];
+        const double alpha = ajj > 0.0 ? -cn : cn;
+        // v = A[j:, j] - alpha e_1;  H = I - 2 v v' / (v'v)
+        const double v0 = ajj - alpha;
+        const double vn2 = 2.0 * cn * (cn + fabs(ajj));   // = v'v, cancellation-free
+        if (vn2 > 0.0) {
+          for (int c = j + 1; c < NW; ++c) {
+            double sd = v0 * A[j * NW + c];
+            for (int t = j + 1; t < n; ++t) sd = fma(A[t * NW + j], A[t * NW + c], sd);
+            const double f = 2.0 * sd / vn2;
+            A[j * NW + c] -= f * v0;
+            for (int t = j + 1; t < n; ++t) A[t * NW + c] = fma(-f, A[t * NW + j], A[t * NW + c]);
+          }
+          double sd = v0 * bb[j];
+          for (int t = j + 1; t < n; ++t) sd = fma(A[t * NW + j], bb[t], sd);
+          const double f = 2.0 * sd / vn2;
+          bb[j] -= f * v0;
+          for (int t = j + 1; t < n; ++t) bb[t] = fma(-f, A[t * NW + j], bb[t]);
+        }
+        A[j * NW + j] = alpha;
+        rank = j + 1;
       }
-      for (int a = 0; a < NW; ++a) {
-        double v = r[a];
-        for (int e = 0; e < a; ++e) v -= N[a][e] * r[e];
-        r[a] = v / N[a][a];
+      for (int a = 0; a < NW; ++a) snu[a] = 0.0;
+      for (int a = rank - 1; a >= 0; --a) {   // R z = Q'b, z -> nu_w[piv]
+        double v = bb[a];
+        for (int e = a + 1; e < rank; ++e) v = fma(-A[a * NW + e], snu[spiv[e]], v);
+        snu[spiv[a]] = v / A[a * NW + a];
       }
-      for (int a = NW - 1; a >= 0; --a) {
-        double v = r[a];
-        for (int e = a + 1; e < NW; ++e) v -= N[e][a] * r[e];
-        r[a] = v / N[a][a];
-      }
-      for (int a = 0; a < NW; ++a) snu[a] = r[a];
     }
   }
   __syncthreads();

@@ -37,7 +37,18 @@ NORM_ACH, ELEM_ACH = 1e-9, 1e-7
 # (Gram-Schmidt in dv and y space) land within 1.7e-8 of the oracle on the worst of
 # 1,024 numpy-restated envs, median 1e-13 -- hence also a median bar.
 WHEEL_NORM, WHEEL_ELEM, WHEEL_MEDIAN = 1e-8, 1e-6, 1e-10
-WHEEL_OK_FRAC = {"standing": 1.0, "tumbling": 0.95}
+# Tumbling envs with the wheel rows: the interior point stalls on ~0.5 % (2,048-env census,
+# tools/wheel_census.py, DESIGN.md §3.1: 9-11 per 2,048 at seeds 86/91/93, 0 standing); every such
+# env is reported OSC_SOLVE_MAX_ITER -- the one non-OK status allowed -- and never returned as OK.
+WHEEL_MAX_ITER_PER_2048 = 16
+
+
+def _wheel_statuses(st, scenario, where):
+    """OK, or MAX_ITER with the census rate bound; standing: OK everywhere."""
+    bad = st != 0
+    assert set(np.unique(st[bad]).tolist()) <= {1}, (where, np.bincount(st))
+    limit = 0 if scenario == "standing" else max(1, WHEEL_MAX_ITER_PER_2048 * len(st) // 2048)
+    assert bad.sum() <= limit, (where, np.bincount(st), np.nonzero(bad)[0][:20])
 # KKT certificate of the GPU's (x, y), each residual scaled as oracle/qp_exact.kkt_certificate.
 # Stationarity: the duals are recovered from x (osc_dual_kernel), so it measures x's optimality
 # through H_dv and M^-1 -- a design vector 1e-9 off in dv shows up as ~1e-8..1e-7 here (WaLTER).
@@ -93,11 +104,9 @@ def test_wheel_rows_vs_oracle(gpu, scenario, mask_mode, seed):
     res = solver("noslip").solve(**d, want_x=True, wheel_dir=wd)
     torch.cuda.synchronize()
     st = res.status.cpu().numpy()
-    # every env converges standing; tumbling (masked wheels, degenerate active sets) a few are
-    # reported as not converged / not refined (DESIGN.md §3.1 measures 0.5-0.7 % of 2,048) --
-    # flagged, never returned as OK: the OK ones are held to the oracle
-    ok_frac = WHEEL_OK_FRAC[scenario]
-    assert (st == 0).mean() >= ok_frac, np.bincount(st)
+    # every env converges standing; tumbling a stalled interior point is flagged MAX_ITER, never
+    # returned as OK: the OK ones are held to the oracle
+    _wheel_statuses(st, scenario, "vs_oracle")
     x = res.x.cpu().numpy()
     ref, viol, envs = [], [], []
     for e in range(nenv):
@@ -283,7 +292,7 @@ def test_wheel_rows_kkt_certificate(gpu):
     s.solve_into(out, *args, wheel_dir=wdt)
     torch.cuda.synchronize()
     st = out.status.cpu().numpy()
-    assert (st == 0).mean() >= 0.98, (np.bincount(st), np.nonzero(st)[0][:20])
+    _wheel_statuses(st, "tumbling", "kkt")
     cert = _kkt(*_batched_qp("walter_sr_wheels", *args, wheel, wdt), out.x, out.y)
     ok = torch.from_numpy(st == 0).cuda()
     # every env reported OK is certified (the rows' multipliers from stationarity itself,
@@ -355,8 +364,9 @@ def test_wheel_rows_warm_start(gpu, scenario, mask_mode):
         s.solve_into(co, *args, wheel_dir=wdt)
         torch.cuda.synchronize()
         sw, sc = wo.status.cpu().numpy(), co.status.cpu().numpy()
+        _wheel_statuses(sw, scenario, ("warm", tick))
+        _wheel_statuses(sc, scenario, ("cold", tick))
         ok = (sw == 0) & (sc == 0)
-        assert ok.mean() >= (1.0 if scenario == "standing" else 0.98), (tick, np.bincount(sw), np.bincount(sc))
         nw, _ = _rel_errors(wo.tau.cpu().numpy()[ok], co.tau.cpu().numpy()[ok])
         assert nw.max() <= WHEEL_NORM, (tick, nw.max())
         if tick > 0:
