@@ -1,6 +1,6 @@
 """Lockstep compaction A/B (ParkArgs in csrc/osc_batch.hip): for each park iteration, the cold
 solve's time per launch (HIP events, median of the timed launches) and a bitwise comparison of
-tau / x / status / iters with compaction off (OSC_PARK_IT=0).
+tau / x / status / iters with compaction off (osc_model_tuning.park_it = 0).
 
     python tools/park_sweep.py ROBOT NENV SCENARIO MASK PARK_IT[,PARK_IT...] [REPS]
 """
@@ -24,8 +24,7 @@ d = generate(robot, nenv, shard_seed(0), scen, mask)
 
 
 def run(park):
-    os.environ["OSC_PARK_IT"] = str(park)
-    s = OSCBatchSolver(robot)
+    s = OSCBatchSolver(robot, tuning={"park_it": park})
     args = s.prepare(**d)
     out = s.alloc_outputs(nenv, want_x=True)
     for _ in range(3):

@@ -3,7 +3,8 @@ OSQP-form KKT certificate of every env reported OK (tests/test_gpu_wheels._kkt),
 not reported OK (or OK but not certified) their status, iterations and torque error against the
 exact oracle.  One parameterised tool in place of round 3's wheel_* one-offs.
 
-    python tools/wheel_census.py [nenv] [seed] [scenario] [mask] [warm_ticks]
+    python tools/wheel_census.py [nenv] [seed] [scenario] [mask] [warm_ticks] [tuning-json] [--brief]
+(--brief: the per-tick summary lines only, no oracle solves)
 """
 import json
 import os
@@ -29,14 +30,19 @@ YAML = os.path.join(os.path.dirname(config_path("walter_sr_wheels")),
 
 
 def main():
+    brief = "--brief" in sys.argv
+    sys.argv = [a for a in sys.argv if a != "--brief"]
     nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     seed = SEED_BASE + (int(sys.argv[2]) if len(sys.argv) > 2 else 86)
     scenario = sys.argv[3] if len(sys.argv) > 3 else "tumbling"
     mask_mode = sys.argv[4] if len(sys.argv) > 4 else "bernoulli"
     ticks = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    tuning = json.loads(sys.argv[6]) if len(sys.argv) > 6 else None
     model = load_model("walter_sr_wheels")
     wheel = WheelRows(dof=np.array(WALTER_WHEEL_DOFS), radius=np.full(8, WHEEL_RADIUS))
-    s = OSCBatchSolver("walter_sr_wheels", YAML)
+    tn = dict(tuning or {})
+    max_iter = tn.pop("max_iter", None)   # (a descriptor field, not osc_model_tuning)
+    s = OSCBatchSolver("walter_sr_wheels", YAML, max_iter=max_iter, tuning=tn or None)
     d = generate("walter_sr_wheels", nenv, seed, scenario, mask_mode)
     rng = np.random.default_rng(seed)
     warm = s.alloc_warm_state(nenv) if ticks > 1 else None
@@ -59,14 +65,14 @@ def main():
             good &= cert[k] <= tol
             worst[k] = float(cert[k][torch.from_numpy(st == 0).cuda()].max().item()) if (st == 0).any() else 0.0
         good = good.cpu().numpy()
-        row = {"tick": tick, "nenv": nenv, "seed": seed, "scenario": scenario,
+        row = {"tick": tick, "nenv": nenv, "seed": seed, "scenario": scenario, "tuning": tuning,
                "status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
                "ok_uncertified": int(((st == 0) & ~good).sum()), "worst_cert_of_ok": worst,
                "iters_mean": float(out.iters.float().mean().item())}
         print(json.dumps(row), flush=True)
         tau = out.tau.cpu().numpy()
         it = out.iters.cpu().numpy()
-        for e in np.nonzero((st != 0) | ~good)[0][:24]:
+        for e in [] if brief else np.nonzero((st != 0) | ~good)[0][:24]:
             a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
             ref = torque(model, solve_exact(model, build_qp(model, *a, wheel, wd[e]), *a[:3]).x)
             err = float(np.abs(tau[e] - ref).max() / max(np.abs(ref).max(), 1.0))
