@@ -56,6 +56,15 @@ def main():
         else:
             s.solve_warm_into(out, warm, *args, wheel_dir=wdt)
         torch.cuda.synchronize()
+        ms = None
+        if brief and warm is None:   # time 10 cold solves of this batch (HIP events)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(10):
+                s.solve_into(out, *args, wheel_dir=wdt)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ms = ev[0].elapsed_time(ev[1]) / 10
         st = out.status.cpu().numpy()
         cert = _kkt(*_batched_qp("walter_sr_wheels", *args, wheel, wdt), out.x, out.y)
         good = torch.ones(nenv, dtype=torch.bool, device=out.x.device)
@@ -68,7 +77,8 @@ def main():
         row = {"tick": tick, "nenv": nenv, "seed": seed, "scenario": scenario, "tuning": tuning,
                "status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
                "ok_uncertified": int(((st == 0) & ~good).sum()), "worst_cert_of_ok": worst,
-               "iters_mean": float(out.iters.float().mean().item())}
+               "iters_mean": float(out.iters.float().mean().item()),
+               "iters_max": int(out.iters.max().item()), "ms": ms}
         print(json.dumps(row), flush=True)
         tau = out.tau.cpu().numpy()
         it = out.iters.cpu().numpy()
