@@ -378,6 +378,16 @@ Status OperationalSpaceController::fetch_outputs_locked() {
   std::memcpy(info, h_out_ + out_doubles_, sizeof(info));
   torque_.assign(h_out_, h_out_ + nu_);                      // = solution[nv : nv+nu] (:573)
   solution_.assign(h_out_ + even(nu_), h_out_ + even(nu_) + n_);
+  // The reference publishes OSQP's solution whatever its exit code (solve_optimization, :531-536,
+  // never reads exit_code); so does this tick -- but a solve that is not OK is reported on stderr
+  // when the status changes, and stays readable through last_solve_status().
+  if (info[0] != OSC_SOLVE_OK && info[0] != status_)
+    std::cerr << "OperationalSpaceController: solve status " << info[0]
+              << (info[0] == OSC_SOLVE_MAX_ITER     ? " (max_iter)"
+                  : info[0] == OSC_SOLVE_NUMERICAL  ? " (non-finite)"
+                  : info[0] == OSC_SOLVE_UNREFINED  ? " (unrefined)"
+                                                    : "")
+              << " after " << info[1] << " iterations; torques published as returned\n";
   status_ = info[0];
   iters_ = info[1];
   return Status::Ok();
