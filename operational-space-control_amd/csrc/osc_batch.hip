@@ -3258,6 +3258,406 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   }
 }
 
+// ==================== kernel 4: wheel-row fallback (Goldfarb-Idnani, optional) ==================
+// An env the wheel-row interior point leaves at max_iter (~0.5 % of tumbling envs: QPs whose
+// multipliers reach 1e7-3e8 -- the rows nearly inconsistent with the torque limits, DESIGN.md
+// §3.1) is solved again by Goldfarb & Idnani's dual active-set method (Math. Programming 27,
+// 1983; quadprog's algorithm, oracle/qp_exact.py::_dual_active_set) on the FULL reference QP of the
+// env (x = (dv, u, z); rows as c'x >= b): start at the unconstrained minimiser, add the equality
+// rows (dynamics, wheel rows, the forces of contacts off the ground), then repeatedly the most
+// violated one-sided row, dropping working rows whose multiplier would turn negative.  Every
+// iterate is dual feasible, so it terminates; J = L^-T Q and R are kept by Givens rotations.
+// tools/gi_fallback_model.py is the numpy restatement of exactly this sequence (its torques are
+// within 1e-11 of the exact oracle on every MAX_ITER env of three 2,048-env censuses).  An env the
+// method certifies (rows held to 1e-8, one-sided rows feasible) reports OK with its x and tau;
+// otherwise it keeps the interior point's result and status.
+// One 64-lane wavefront per env, early exit for envs already OK.  Lanes own J's rows (row i of
+// J = lane i), the working set's multipliers and row ids (lane j = position j), and the
+// one-sided rows (lane p = row p) for the violation scan.
+template <class D>
+__global__ __launch_bounds__(kWave) void osc_gi_kernel(
+    const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
+    const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
+    const double* __restrict__ gmask, const double* __restrict__ gwd,
+    const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
+    int32_t* __restrict__ gstatus) {
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NW = D::NW, NX = D::NX,
+                NB = D::NB, NZ = D::NZ;
+  constexpr int NXP = NX | 1;                 // odd row stride (LDS banks)
+  constexpr int NEQ = NV + NW + NZ;           // dynamics, wheel rows, forces of masked contacts
+  constexpr int NIN = 2 * NU + 6 * NC;        // one-sided rows: u box, pyramid, fz box
+  constexpr int JC0 = 3 * (NS - NC);          // first contact translational row of J
+  constexpr int kIneq = 1 << 12;              // row ids: equality k, one-sided kIneq + p
+  constexpr int kMaxSteps = 400;
+  static_assert(NX <= kWave && NIN <= kWave && NEQ <= kWave, "one lane per variable / row");
+  const int env = static_cast<int>(blockIdx.x), lane = static_cast<int>(threadIdx.x);
+  if (env >= nenv) return;
+  if (gstatus[env] == OSC_SOLVE_OK) return;   // (block-uniform)
+  __shared__ double sE[NEQ * NXP];            // equality rows, dense
+  __shared__ double sEb[NEQ];
+  __shared__ double sJ[NX * NXP];             // J (row i at i * NXP); first the Cholesky factor
+  __shared__ double sR[NX * NXP];             // R, upper triangular (row i at i * NXP)
+  __shared__ double sx[NX], sc[NX], sd[NX], sgc[NX], sgs[NX];
+  const double* wenv = ws + static_cast<size_t>(env) * D::WS;
+  const double* M = gM + static_cast<size_t>(env) * NV * NV;
+  const double* C = gC + static_cast<size_t>(env) * NV;
+  const double* J = gJ + static_cast<size_t>(env) * D::S * NV;
+  const double* bb = gb + static_cast<size_t>(env) * D::S;
+  const double* mask = gmask + static_cast<size_t>(env) * NC;
+  const double* wd = gwd + static_cast<size_t>(env) * NC * 6;
+  const double hu = 2.0 * (P->w_torque + P->w_reg), hz = 2.0 * P->w_reg;
+
+  auto wsum = [](double v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+  };
+  auto wmax = [](double v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    return v;
+  };
+  // (value, index) minimum, the lowest index among ties
+  auto wargmin = [](double& v, int& idx) {
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o, kWave);
+      const int oi = __shfl_xor(idx, o, kWave);
+      if (ov < v || (ov == v && oi < idx)) {
+        v = ov;
+        idx = oi;
+      }
+    }
+  };
+  // one-sided row p (c'x >= b): its coefficient on variable i, right-hand side, max |c|, and
+  // whether it exists (finite bound; the fz box only on contacts in touch)
+  auto in_coef = [&](int p, int i) -> double {
+    if (p < 2 * NU) return (i == NV + p / 2) ? ((p & 1) ? 1.0 : -1.0) : 0.0;
+    const int k = (p - 2 * NU) / 6, r = (p - 2 * NU) % 6, c0 = NV + NU + 3 * k;
+    if (i < c0 || i >= c0 + 3) return 0.0;
+    if (r < 4) {   // (sx, sy, -mu) z <= 0 (autogen.py:112-117 order)
+      const double sx = (r & 1) ? -1.0 : 1.0, sy = (r >= 2) ? -1.0 : 1.0;
+      return i == c0 ? -sx : (i == c0 + 1 ? -sy : P->mu);
+    }
+    return i == c0 + 2 ? (r == 4 ? 1.0 : -1.0) : 0.0;
+  };
+  auto in_rhs = [&](int p) -> double {
+    if (p < 2 * NU) return (p & 1) ? P->u_lb[p / 2] : -P->u_ub[p / 2];
+    const int k = (p - 2 * NU) / 6, r = (p - 2 * NU) % 6;
+    return r < 4 ? 0.0 : (r == 4 ? P->z_lb[2] * mask[k] : -P->z_ub[2] * mask[k]);
+  };
+  auto in_valid = [&](int p) -> bool {
+    if (p >= NIN) return false;
+    if (p < 2 * NU) return fabs((p & 1) ? P->u_lb[p / 2] : P->u_ub[p / 2]) < P->inf_thresh;
+    const int k = (p - 2 * NU) / 6, r = (p - 2 * NU) % 6;
+    if (r < 4) return true;
+    return mask[k] != 0.0 && fabs(r == 4 ? P->z_lb[2] : P->z_ub[2]) < P->inf_thresh;
+  };
+  auto in_scale = [&](int p) -> double {
+    return (p >= 2 * NU && (p - 2 * NU) % 6 < 4) ? fmax(1.0, fabs(P->mu)) : 1.0;
+  };
+
+  // ---- the equality rows (the reference's Aeq = [M, -B, -Jc], beq = -C; its wheel rows; z = 0
+  // on contacts off the ground) ----
+  int neq = 0;
+  for (int i = 0; i < NV; ++i) {
+    if (lane < NX) {
+      double v;
+      if (lane < NV) v = M[i * NV + lane];
+      else if (lane < NV + NU) v = (i == NB + lane - NV) ? -1.0 : 0.0;
+      else v = -J[(JC0 + lane - NV - NU) * NV + i];
+      sE[neq * NXP + lane] = v;
+    }
+    if (lane == 0) sEb[neq] = -C[i];
+    ++neq;
+  }
+  for (int w = 0; w < NW; ++w) {   // osc_qp.wheel_rows (walter_sr_wheels/autogen.py:151-205)
+    const int i = w / 2, side = w % 2;
+    if (lane < NX) {
+      double v = 0.0;
+      if (lane < NV) {
+        for (int c = 0; c < 3; ++c) v = fma(wd[6 * i + 3 * side + c], J[(JC0 + 3 * i + c) * NV + lane], v);
+        if (side == 0 && lane == P->wheel_dof[i]) v -= P->wheel_radius[i];
+        v *= mask[i];
+      }
+      sE[neq * NXP + lane] = v;
+    }
+    if (lane == 0) {
+      double e = 0.0;
+      for (int c = 0; c < 3; ++c) e = fma(wd[6 * i + 3 * side + c], bb[JC0 + 3 * i + c], e);
+      sEb[neq] = -mask[i] * e;
+    }
+    ++neq;
+  }
+  for (int k = 0; k < NC; ++k) {
+    if (mask[k] != 0.0) continue;
+    for (int c = 0; c < 3; ++c) {
+      if (lane < NX) sE[neq * NXP + lane] = (lane == NV + NU + 3 * k + c) ? 1.0 : 0.0;
+      if (lane == 0) sEb[neq] = 0.0;
+      ++neq;
+    }
+  }
+
+  // ---- H = blockdiag(H_dv, hu I, hz I) = L L';  J = L^-T;  x = -H^-1 f ----
+  for (int p = lane; p < NV * NV; p += kWave) sR[(p / NV) * NXP + p % NV] = wenv[D::W_HD + p];
+  __syncthreads();
+  for (int k = 0; k < NV; ++k) {   // left-looking Cholesky of H_dv in sR, lane = row
+    double t = 0.0;
+    if (lane >= k && lane < NV) {
+      t = sR[lane * NXP + k];
+      for (int p = 0; p < k; ++p) t = fma(-sR[lane * NXP + p], sR[k * NXP + p], t);
+      sR[lane * NXP + k] = t;
+    }
+    __syncthreads();
+    const double dk = sqrt(sR[k * NXP + k]);
+    __syncthreads();
+    if (lane >= k && lane < NV) sR[lane * NXP + k] = (lane == k) ? dk : t / dk;
+    __syncthreads();
+  }
+  if (lane < NX) {
+    // lane j: column j of L^-1 (forward substitution of e_j) = row j of J = L^-T
+    for (int c = 0; c < NX; ++c) sJ[lane * NXP + c] = 0.0;
+    if (lane < NV) {
+      double y[NV];
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        double a = (r == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < r; ++k) a = fma(-sR[r * NXP + k], y[k], a);
+        y[r] = a / sR[r * NXP + r];
+      }
+#pragma unroll
+      for (int r = 0; r < NV; ++r) sJ[lane * NXP + r] = y[r];
+    } else {
+      sJ[lane * NXP + lane] = 1.0 / sqrt(lane < NV + NU ? hu : hz);
+    }
+  }
+  __syncthreads();
+  for (int p = lane; p < NX * NXP; p += kWave) sR[p] = 0.0;
+  // x_dv = -J_dv J_dv' f_dv; u = z = 0
+  if (lane < NX) sc[lane] = lane < NV ? wenv[D::W_GD + lane] : 0.0;
+  __syncthreads();
+  if (lane < NX) {
+    double t = 0.0;
+    for (int i = 0; i < NX; ++i) t = fma(sJ[i * NXP + lane], sc[i], t);
+    sd[lane] = t;
+  }
+  __syncthreads();
+  double xi = 0.0;   // lane i: x_i
+  if (lane < NX) {
+    for (int j = 0; j < NX; ++j) xi = fma(-sJ[lane * NXP + j], sd[j], xi);
+    sx[lane] = xi;
+  }
+  // the dependence test's scale: J's largest row norm (invariant under J <- J Q)
+  double rn = 0.0;
+  if (lane < NX)
+    for (int c = 0; c < NX; ++c) rn = fma(sJ[lane * NXP + c], sJ[lane * NXP + c], rn);
+  const double jscale = sqrt(wmax(rn));
+  __syncthreads();
+
+  int q = 0;            // working rows
+  int act = -1;         // lane j < q: row id of working row j
+  double up = 0.0;      // lane j <= q: multipliers (j = q: the candidate's)
+  double zi = 0.0;      // lane i: the primal step direction z
+  double rj = 0.0;      // lane j < q: R^-1 d[:q]
+  // d = J'c (lane j -> sd), z = J[:, q:] d[q:] (lane i), r = R^-1 d[:q] (lane j); c in sc
+  auto directions = [&]() {
+    if (lane < NX) {
+      double t = 0.0;
+      for (int i = 0; i < NX; ++i) t = fma(sJ[i * NXP + lane], sc[i], t);
+      sd[lane] = t;
+    }
+    __syncthreads();
+    zi = 0.0;
+    if (lane < NX)
+      for (int j = q; j < NX; ++j) zi = fma(sJ[lane * NXP + j], sd[j], zi);
+    double dv = lane < q ? sd[lane] : 0.0;
+    rj = 0.0;
+    for (int jj = q - 1; jj >= 0; --jj) {   // back substitution, column-oriented
+      const double v = __shfl(dv, jj, kWave) / sR[jj * NXP + jj];
+      if (lane == jj) rj = v;
+      if (lane < jj) dv = fma(-sR[lane * NXP + jj], v, dv);
+    }
+  };
+  // c joins the working set at position q: rotate d[q+1:] into d[q] (J's columns follow), R's
+  // column q = d[:q+1]
+  auto add_row = [&]() {
+    if (lane == 0) {
+      for (int j = NX - 1; j > q; --j) {
+        const double a = sd[j - 1], b = sd[j];
+        double c = 1.0, s = 0.0, r = a;
+        if (b != 0.0) {
+          r = hypot(a, b);
+          c = a / r;
+          s = b / r;
+        }
+        sd[j - 1] = r;
+        sd[j] = 0.0;
+        sgc[j] = c;
+        sgs[j] = s;
+      }
+    }
+    __syncthreads();
+    if (lane < NX) {
+      for (int j = NX - 1; j > q; --j) {
+        const double c = sgc[j], s = sgs[j];
+        const double a = sJ[lane * NXP + j - 1], b = sJ[lane * NXP + j];
+        sJ[lane * NXP + j - 1] = c * a + s * b;
+        sJ[lane * NXP + j] = -s * a + c * b;
+      }
+    }
+    if (lane <= q) sR[lane * NXP + q] = sd[lane];
+    __syncthreads();
+  };
+  // working row k leaves: R's columns k+1.. shift left and are re-triangularised by rotations of
+  // rows (j, j+1), J's columns (j, j+1) follow; the lanes' ids / multipliers shift down
+  auto drop_row = [&](int k) {
+    if (lane < q)
+      for (int c = k; c < q - 1; ++c) sR[lane * NXP + c] = sR[lane * NXP + c + 1];
+    if (lane < NX) sR[lane * NXP + q - 1] = 0.0;
+    __syncthreads();
+    for (int j = k; j < q - 1; ++j) {
+      const double a = sR[j * NXP + j], b = sR[(j + 1) * NXP + j];
+      double c = 1.0, s = 0.0;
+      if (b != 0.0) {
+        const double r = hypot(a, b);
+        c = a / r;
+        s = b / r;
+      }
+      __syncthreads();
+      if (lane >= j && lane < q - 1) {
+        const double ra = sR[j * NXP + lane], rb = sR[(j + 1) * NXP + lane];
+        sR[j * NXP + lane] = c * ra + s * rb;
+        sR[(j + 1) * NXP + lane] = -s * ra + c * rb;
+      }
+      if (lane == 0) {
+        sgc[j] = c;
+        sgs[j] = s;
+      }
+      __syncthreads();
+    }
+    if (lane < NX) sR[(q - 1) * NXP + lane] = 0.0;
+    if (lane < NX) {
+      for (int j = k; j < q - 1; ++j) {
+        const double c = sgc[j], s = sgs[j];
+        const double a = sJ[lane * NXP + j], b = sJ[lane * NXP + j + 1];
+        sJ[lane * NXP + j] = c * a + s * b;
+        sJ[lane * NXP + j + 1] = -s * a + c * b;
+      }
+    }
+    const int na = __shfl_down(act, 1, kWave);
+    const double nu_ = __shfl_down(up, 1, kWave);
+    if (lane >= k && lane < q) {
+      act = na;
+      up = nu_;
+    }
+    if (lane == q) up = 0.0;
+    __syncthreads();
+  };
+
+  bool ok = true;
+  int steps = 0;
+  // ---- equality rows: always in, never dropped; a row dependent on those already in skipped ----
+  for (int k = 0; k < neq && ok; ++k) {
+    const double ck = lane < NX ? sE[k * NXP + lane] : 0.0;
+    if (lane < NX) sc[lane] = ck;
+    __syncthreads();
+    directions();
+    const double zmax = wmax(fabs(zi)), cmax = wmax(fabs(ck));
+    if (zmax <= 1e-13 * cmax * (1.0 + jscale)) continue;
+    const double cx = wsum(ck * xi), zc = wsum(zi * ck);
+    const double t = (sEb[k] - cx) / zc;
+    if (!isfinite(t)) { ok = false; break; }
+    xi = fma(t, zi, xi);
+    if (lane < q) up = fma(-t, rj, up);
+    if (lane == q) { up = t; act = k; }
+    add_row();
+    ++q;
+  }
+  if (lane < NX) sx[lane] = xi;
+  __syncthreads();
+  // ---- one-sided rows ----
+  while (ok) {
+    if (++steps > kMaxSteps) { ok = false; break; }
+    // working one-sided rows as a bit set over p
+    unsigned long long in_set = (lane < q && act >= kIneq) ? (1ull << (act - kIneq)) : 0ull;
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const unsigned lo = __shfl_xor(static_cast<unsigned>(in_set), o, kWave);
+      const unsigned hi = __shfl_xor(static_cast<unsigned>(in_set >> 32), o, kWave);
+      in_set |= (static_cast<unsigned long long>(hi) << 32) | lo;
+    }
+    const double xs = wmax(lane < NX ? fabs(xi) : 0.0);
+    double viol = INFINITY;
+    int p = lane;
+    if (in_valid(lane) && !((in_set >> lane) & 1ull)) {
+      double s = -in_rhs(lane);
+      for (int i = 0; i < NX; ++i) {
+        const double cf = in_coef(lane, i);
+        if (cf != 0.0) s = fma(cf, sx[i], s);
+      }
+      viol = s / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane)));
+    }
+    wargmin(viol, p);
+    if (!(viol < -1e-14)) break;   // every one-sided row holds: optimal
+    const double cp = lane < NX ? in_coef(p, lane) : 0.0;
+    const double bp = in_rhs(p), scp = in_scale(p);
+    if (lane < NX) sc[lane] = cp;
+    __syncthreads();
+    if (lane == q) up = 0.0;
+    while (true) {
+      if (++steps > kMaxSteps) { ok = false; break; }
+      directions();
+      // partial step: the working one-sided row whose multiplier reaches 0 first
+      const double rmax = 1.0 + wmax(lane < q ? fabs(rj) : 0.0);
+      double t1 = INFINITY;
+      int kd = lane;
+      if (lane < q && act >= kIneq && rj > 1e-14 * rmax) t1 = up / rj;
+      wargmin(t1, kd);
+      const double zmax = wmax(fabs(zi));
+      const bool dependent = zmax <= 1e-13 * scp * (1.0 + jscale);
+      const double cx = wsum(cp * xi), zc = wsum(zi * cp);
+      const double t2 = dependent ? INFINITY : -(cx - bp) / zc;
+      const double t = fmin(t1, t2);
+      if (!isfinite(t)) { ok = false; break; }
+      if (!dependent) xi = fma(t, zi, xi);
+      if (lane < q) up = fma(-t, rj, up);
+      if (lane == q) up += t;
+      if (lane < NX) sx[lane] = xi;
+      __syncthreads();
+      if (t2 <= t1) {   // full step: p joins
+        if (lane == q) act = kIneq + p;
+        add_row();
+        ++q;
+        break;
+      }
+      drop_row(kd);
+      --q;
+    }
+  }
+  if (!ok) return;
+  // ---- certify: every equality row held, every one-sided row feasible ----
+  const double xs = wmax(lane < NX ? fabs(xi) : 0.0);
+  double bad = 0.0;
+  if (lane < neq) {
+    double s = -sEb[lane], cm = 0.0;
+    for (int i = 0; i < NX; ++i) {
+      s = fma(sE[lane * NXP + i], sx[i], s);
+      cm = fmax(cm, fabs(sE[lane * NXP + i]));
+    }
+    bad = fabs(s) / (1.0 + cm * xs + fabs(sEb[lane])) <= 1e-8 ? 0.0 : 1.0;   // (NaN: bad)
+  }
+  if (lane < NX && !isfinite(xi)) bad = 1.0;
+  if (in_valid(lane)) {
+    double s = -in_rhs(lane);
+    for (int i = 0; i < NX; ++i) {
+      const double cf = in_coef(lane, i);
+      if (cf != 0.0) s = fma(cf, sx[i], s);
+    }
+    if (!(s / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane))) >= -1e-9)) bad = 1.0;
+  }
+  if (!(wmax(bad) == 0.0) || !isfinite(xs)) return;
+  if (gx != nullptr && lane < NX) gx[static_cast<size_t>(env) * NX + lane] = xi;
+  if (lane >= NV && lane < NV + NU) gtau[static_cast<size_t>(env) * NU + lane - NV] = xi;
+  if (lane == 0) gstatus[env] = OSC_SOLVE_OK;
+}
+
 using Go2 = Dims<18, 12, 4, 5>;   // unitree_go2: nv 18, nu 12, 4 feet, 5 sites
 using Walter = Dims<14, 8, 8, 17>;   // walter_sr(_wheels): nv 14, nu 8, 8 wheels, 17 sites
 using WalterW = Dims<14, 8, 8, 17, true>;   // + the wheel no-slip rows (opt-in)
@@ -3565,16 +3965,23 @@ void launch_t(const osc_model* model, int32_t nenv, const double* M, const doubl
     // wheel rows: the one-wave solve with the refinement fused (launch() checked the rest); warm-
     // started: the warm pass, then the cold fix-up pass over the wavefronts holding an env the
     // warm start left unconverged (the per-env status: the caller's array, else scratch)
+    // The fused entries (raw inputs at hand) then run the active-set fallback over the envs the
+    // interior point left unconverged (osc_gi_kernel); it needs the per-env status too.
+    const bool fallback = M && C && J && b && wdir;
+    if (status == nullptr && (warm != nullptr || fallback))
+      status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
     if (warm == nullptr) {
       hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
                          model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
     } else {
-      if (status == nullptr) status = reinterpret_cast<int32_t*>(ws + static_cast<size_t>(D::WS) * nenv);
       for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, warm,
                            flags | pass);
     }
+    if (fallback)
+      hipLaunchKernelGGL(osc_gi_kernel<D>, dim3(static_cast<unsigned>(nenv)), dim3(kWave), 0, s,
+                         model->dparams, nenv, M, C, J, b, mask, wdir, ws, tau, x, status);
   } else {
     // A warm-started solve is followed by a cold fix-up pass over the wavefronts that hold an
     // env the warm start did not bring to convergence (it needs the per-env status: the

@@ -1,0 +1,160 @@
+"""Numpy model of the wheel-row fallback kernel (osc_batch.hip, osc_gi_kernel): Goldfarb & Idnani's
+dual active-set method on the FULL QP of one env (x = (dv, u, z), the reference's rows) for the
+envs the interior point leaves at max_iter.  The same algorithm and update order as the kernel --
+J = L^-T Q and R kept by Givens rotations, equality rows first (never dropped), then the most
+violated one-sided row -- so its iterates can be compared step by step.  Not product code.
+
+    python tools/gi_fallback_model.py SEED_OFFSET CENSUS_JSONL     (MAX_ITER envs of a census)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in ("operational-space-control_amd", "oracle"):
+    sys.path.insert(0, os.path.join(REPO, p))
+from osc_qp import OSQP_INFTY, WheelRows, build_qp, load_model, torque  # noqa: E402
+
+
+def givens(a, b):
+    if b == 0.0:
+        return 1.0, 0.0, a
+    r = np.hypot(a, b)
+    return a / r, b / r, r
+
+
+def rows_of(qp, n):
+    """(normals c, rhs b, is_equality) with rows as c'x >= b (equalities c'x = b)."""
+    cs, bs, eqs = [], [], []
+    A, l, u = qp.A, qp.l, qp.u
+    for i in range(A.shape[0]):
+        lo, hi = l[i] > -OSQP_INFTY / 2, u[i] < OSQP_INFTY / 2
+        if lo and hi and l[i] == u[i]:
+            cs.append(A[i]); bs.append(u[i]); eqs.append(True)
+            continue
+        if hi:
+            cs.append(-A[i]); bs.append(-u[i]); eqs.append(False)
+        if lo:
+            cs.append(A[i]); bs.append(l[i]); eqs.append(False)
+    order = sorted(range(len(cs)), key=lambda k: not eqs[k])   # equalities first
+    return ([cs[k] for k in order], np.array([bs[k] for k in order]),
+            np.array([eqs[k] for k in order]))
+
+
+def gi_full(H, f, cs, bs, eqs, max_steps=400):
+    n = H.shape[0]
+    L = np.linalg.cholesky(H)
+    Jm = np.linalg.inv(L).T
+    x = -np.linalg.solve(H, f)
+    R = np.zeros((n, n))
+    act: list[int] = []
+    u = np.zeros(0)
+    neq = int(eqs.sum())
+    steps = 0
+    # the dependence test's scale: J's largest row norm (invariant under the rotations J <- J Q)
+    jscale = np.linalg.norm(Jm, axis=1).max()
+
+    def add(d, q):
+        nonlocal Jm
+        for j in range(n - 1, q, -1):
+            c, s, r = givens(d[j - 1], d[j])
+            d[j - 1], d[j] = r, 0.0
+            a, b = Jm[:, j - 1].copy(), Jm[:, j].copy()
+            Jm[:, j - 1], Jm[:, j] = c * a + s * b, -s * a + c * b
+        R[:q + 1, q] = d[:q + 1]
+
+    def drop(k, q):
+        nonlocal Jm
+        R[:q, k:q - 1] = R[:q, k + 1:q].copy()
+        R[:, q - 1] = 0.0
+        for j in range(k, q - 1):
+            c, s, r = givens(R[j, j], R[j + 1, j])
+            a, b = R[j, j:q - 1].copy(), R[j + 1, j:q - 1].copy()
+            R[j, j:q - 1], R[j + 1, j:q - 1] = c * a + s * b, -s * a + c * b
+            a, b = Jm[:, j].copy(), Jm[:, j + 1].copy()
+            Jm[:, j], Jm[:, j + 1] = c * a + s * b, -s * a + c * b
+        R[q - 1, :] = 0.0
+
+    for k in range(neq):
+        c = cs[k]
+        q = len(act)
+        d = Jm.T @ c
+        z = Jm[:, q:] @ d[q:]
+        if np.abs(z).max() <= 1e-13 * np.abs(c).max() * (1.0 + jscale):
+            continue
+        r = np.linalg.solve(R[:q, :q], d[:q]) if q else np.zeros(0)
+        t = (bs[k] - c @ x) / (z @ c)
+        x = x + t * z
+        u = np.append(u - t * r, t)
+        add(d, q)
+        act.append(k)
+    scale = np.array([np.abs(c).max() for c in cs])
+    while True:
+        steps += 1
+        if steps > max_steps:
+            return x, act, steps, False
+        xs = np.abs(x).max()
+        s = np.array([cs[k] @ x - bs[k] for k in range(len(cs))])
+        viol = s / (1.0 + scale * xs + np.abs(bs))
+        viol[:neq] = np.inf
+        viol[act] = np.inf
+        p = int(np.argmin(viol))
+        if viol[p] >= -1e-14:
+            return x, act, steps, True
+        c = cs[p]
+        up = np.append(u, 0.0)
+        while True:
+            q = len(act)
+            d = Jm.T @ c
+            z = Jm[:, q:] @ d[q:]
+            r = np.linalg.solve(R[:q, :q], d[:q]) if q else np.zeros(0)
+            t1, kdrop = np.inf, -1
+            rmax = 1.0 + (np.abs(r).max() if q else 0.0)
+            for j in range(q):
+                if act[j] >= neq and r[j] > 1e-14 * rmax and up[j] / r[j] < t1:
+                    t1, kdrop = up[j] / r[j], j
+            dependent = np.abs(z).max() <= 1e-13 * scale[p] * (1.0 + jscale)
+            t2 = np.inf if dependent else -(c @ x - bs[p]) / (z @ c)
+            t = min(t1, t2)
+            if not np.isfinite(t):
+                return x, act, steps, False
+            if not dependent:
+                x = x + t * z
+            up[:q] -= t * r
+            up[q] += t
+            if t2 <= t1:
+                add(d, q)
+                act.append(p)
+                u = up
+                break
+            drop(kdrop, q)
+            del act[kdrop]
+            up = np.delete(up, kdrop)
+
+
+def main():
+    from osc_amd.synth import SEED_BASE, WALTER_WHEEL_DOFS, WHEEL_RADIUS, generate, wheel_directions
+    from qp_exact import solve_exact
+    model = load_model("walter_sr_wheels")
+    wheel = WheelRows(dof=np.array(WALTER_WHEEL_DOFS), radius=np.full(8, WHEEL_RADIUS))
+    seed = SEED_BASE + int(sys.argv[1])
+    d = generate("walter_sr_wheels", 2048, seed, "tumbling", "bernoulli")
+    wd = wheel_directions("walter_sr_wheels", d, wheel.dof, wheel.radius, seed + 1)
+    envs = sorted({json.loads(l)["env"] for l in open(sys.argv[2]) if '"env"' in l})
+    envs += list(range(0, 64, 9))
+    for e in envs:
+        a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        qp = build_qp(model, *a, wheel, wd[e])
+        cs, bs, eqs = rows_of(qp, model.n)
+        x, act, steps, ok = gi_full(qp.H, qp.f, cs, bs, eqs)
+        ref = torque(model, solve_exact(model, qp, *a[:3]).x)
+        err = np.abs(torque(model, x) - ref).max() / max(np.abs(ref).max(), 1.0)
+        print(json.dumps({"env": e, "ok": ok, "steps": steps, "active": len(act), "err": err}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
