@@ -3350,6 +3350,14 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     if (r < 4) return true;
     return mask[k] != 0.0 && fabs(r == 4 ? P->z_lb[2] : P->z_ub[2]) < P->inf_thresh;
   };
+  // c_p'x - b_p from the current x in sx (the row's <= 3 nonzeros)
+  auto in_slack = [&](int p) -> double {
+    double v = -in_rhs(p);
+    if (p < 2 * NU) return fma(in_coef(p, NV + p / 2), sx[NV + p / 2], v);
+    const int c0 = NV + NU + 3 * ((p - 2 * NU) / 6);
+    for (int i = c0; i < c0 + 3; ++i) v = fma(in_coef(p, i), sx[i], v);
+    return v;
+  };
   auto in_scale = [&](int p) -> double {
     return (p >= 2 * NU && (p - 2 * NU) % 6 < 4) ? fmax(1.0, fabs(P->mu)) : 1.0;
   };
@@ -3457,17 +3465,42 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   double up = 0.0;      // lane j <= q: multipliers (j = q: the candidate's)
   double zi = 0.0;      // lane i: the primal step direction z
   double rj = 0.0;      // lane j < q: R^-1 d[:q]
-  // d = J'c (lane j -> sd), z = J[:, q:] d[q:] (lane i), r = R^-1 d[:q] (lane j); c in sc
-  auto directions = [&]() {
+  // d = J'c (lane j -> sd), z = J[:, q:] d[q:] (lane i), r = R^-1 d[:q] (lane j).  c: a dense
+  // equality row in sc, or one-sided row p (<= 3 nonzeros: only those rows of J are read)
+  auto directions = [&](int p) {
     if (lane < NX) {
       double t = 0.0;
-      for (int i = 0; i < NX; ++i) t = fma(sJ[i * NXP + lane], sc[i], t);
+      if (p < 0) {
+        double t1 = 0.0, t2 = 0.0, t3 = 0.0;
+        int i = 0;
+        for (; i + 3 < NX; i += 4) {
+          t = fma(sJ[i * NXP + lane], sc[i], t);
+          t1 = fma(sJ[(i + 1) * NXP + lane], sc[i + 1], t1);
+          t2 = fma(sJ[(i + 2) * NXP + lane], sc[i + 2], t2);
+          t3 = fma(sJ[(i + 3) * NXP + lane], sc[i + 3], t3);
+        }
+        for (; i < NX; ++i) t = fma(sJ[i * NXP + lane], sc[i], t);
+        t = (t + t1) + (t2 + t3);
+      } else if (p < 2 * NU) {
+        t = in_coef(p, NV + p / 2) * sJ[(NV + p / 2) * NXP + lane];
+      } else {
+        const int c0 = NV + NU + 3 * ((p - 2 * NU) / 6);
+        for (int i = c0; i < c0 + 3; ++i) t = fma(in_coef(p, i), sJ[i * NXP + lane], t);
+      }
       sd[lane] = t;
     }
     __syncthreads();
     zi = 0.0;
-    if (lane < NX)
-      for (int j = q; j < NX; ++j) zi = fma(sJ[lane * NXP + j], sd[j], zi);
+    if (lane < NX) {
+      double z1 = 0.0;
+      int j = q;
+      for (; j + 1 < NX; j += 2) {
+        zi = fma(sJ[lane * NXP + j], sd[j], zi);
+        z1 = fma(sJ[lane * NXP + j + 1], sd[j + 1], z1);
+      }
+      if (j < NX) zi = fma(sJ[lane * NXP + j], sd[j], zi);
+      zi += z1;
+    }
     double dv = lane < q ? sd[lane] : 0.0;
     rj = 0.0;
     for (int jj = q - 1; jj >= 0; --jj) {   // back substitution, column-oriented
@@ -3476,34 +3509,49 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       if (lane < jj) dv = fma(-sR[lane * NXP + jj], v, dv);
     }
   };
-  // c joins the working set at position q: rotate d[q+1:] into d[q] (J's columns follow), R's
-  // column q = d[:q+1]
+  // c joins the working set at position q: the rotations (j-1, j), j = NX-1 .. q+1, that fold
+  // d[q+1:] into d[q] (J's columns follow); rotation j meets (d[j-1], ||d[j:]||) -- d[NX-1] itself,
+  // signed, for the first -- so every (c, s) follows from d's suffix sums of squares, one wave
+  // scan instead of a chain of NX - q dependent rotations.  R's column q = d[:q+1].
   auto add_row = [&]() {
-    if (lane == 0) {
-      for (int j = NX - 1; j > q; --j) {
-        const double a = sd[j - 1], b = sd[j];
-        double c = 1.0, s = 0.0, r = a;
-        if (b != 0.0) {
-          r = hypot(a, b);
-          c = a / r;
-          s = b / r;
-        }
-        sd[j - 1] = r;
-        sd[j] = 0.0;
-        sgc[j] = c;
-        sgs[j] = s;
-      }
+    const double dl = lane < NX ? sd[lane] : 0.0;
+    double ssq = (lane >= q && lane < NX) ? dl * dl : 0.0;
+    for (int o = 1; o < kWave; o <<= 1) {   // suffix sums S_j = sum_{k >= j} d_k^2
+      const double v = __shfl_down(ssq, o, kWave);
+      if (lane + o < kWave) ssq += v;
     }
+    const double sn = __shfl_down(ssq, 1, kWave);            // S_{j+1} on lane j
+    const double dnext = __shfl_down(dl, 1, kWave);          // d_{j+1} on lane j
+    if (lane >= q && lane < NX - 1) {   // lane j - 1 holds rotation j's (c, s)
+      const double rr = sqrt(ssq);
+      double c = 1.0, sv = 0.0;
+      if (rr > 0.0) {
+        c = dl / rr;
+        sv = (lane + 1 == NX - 1 ? dnext : sqrt(sn)) / rr;
+      }
+      sgc[lane + 1] = c;
+      sgs[lane + 1] = sv;
+    }
+    const double dq = __shfl(q < NX - 1 ? sqrt(ssq) : dl, q, kWave);
     __syncthreads();
     if (lane < NX) {
-      for (int j = NX - 1; j > q; --j) {
-        const double c = sgc[j], s = sgs[j];
-        const double a = sJ[lane * NXP + j - 1], b = sJ[lane * NXP + j];
-        sJ[lane * NXP + j - 1] = c * a + s * b;
-        sJ[lane * NXP + j] = -s * a + c * b;
+      double row[NX];
+#pragma unroll
+      for (int c = 0; c < NX; ++c) row[c] = sJ[lane * NXP + c];
+#pragma unroll
+      for (int j = NX - 1; j >= 1; --j) {
+        if (j > q) {
+          const double c = sgc[j], sv = sgs[j];
+          const double a = row[j - 1], b = row[j];
+          row[j - 1] = c * a + sv * b;
+          row[j] = -sv * a + c * b;
+        }
       }
+#pragma unroll
+      for (int c = 0; c < NX; ++c) sJ[lane * NXP + c] = row[c];
     }
-    if (lane <= q) sR[lane * NXP + q] = sd[lane];
+    if (lane < q) sR[lane * NXP + q] = dl;
+    if (lane == q) sR[q * NXP + q] = dq;
     __syncthreads();
   };
   // working row k leaves: R's columns k+1.. shift left and are re-triangularised by rotations of
@@ -3559,7 +3607,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     const double ck = lane < NX ? sE[k * NXP + lane] : 0.0;
     if (lane < NX) sc[lane] = ck;
     __syncthreads();
-    directions();
+    directions(-1);
     const double zmax = wmax(fabs(zi)), cmax = wmax(fabs(ck));
     if (zmax <= 1e-13 * cmax * (1.0 + jscale)) continue;
     const double cx = wsum(ck * xi), zc = wsum(zi * ck);
@@ -3586,14 +3634,8 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     const double xs = wmax(lane < NX ? fabs(xi) : 0.0);
     double viol = INFINITY;
     int p = lane;
-    if (in_valid(lane) && !((in_set >> lane) & 1ull)) {
-      double s = -in_rhs(lane);
-      for (int i = 0; i < NX; ++i) {
-        const double cf = in_coef(lane, i);
-        if (cf != 0.0) s = fma(cf, sx[i], s);
-      }
-      viol = s / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane)));
-    }
+    if (in_valid(lane) && !((in_set >> lane) & 1ull))
+      viol = in_slack(lane) / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane)));
     wargmin(viol, p);
     if (!(viol < -1e-14)) break;   // every one-sided row holds: optimal
     const double cp = lane < NX ? in_coef(p, lane) : 0.0;
@@ -3603,7 +3645,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     if (lane == q) up = 0.0;
     while (true) {
       if (++steps > kMaxSteps) { ok = false; break; }
-      directions();
+      directions(p);
       // partial step: the working one-sided row whose multiplier reaches 0 first
       const double rmax = 1.0 + wmax(lane < q ? fabs(rj) : 0.0);
       double t1 = INFINITY;
@@ -3644,14 +3686,9 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     bad = fabs(s) / (1.0 + cm * xs + fabs(sEb[lane])) <= 1e-8 ? 0.0 : 1.0;   // (NaN: bad)
   }
   if (lane < NX && !isfinite(xi)) bad = 1.0;
-  if (in_valid(lane)) {
-    double s = -in_rhs(lane);
-    for (int i = 0; i < NX; ++i) {
-      const double cf = in_coef(lane, i);
-      if (cf != 0.0) s = fma(cf, sx[i], s);
-    }
-    if (!(s / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane))) >= -1e-9)) bad = 1.0;
-  }
+  if (in_valid(lane) &&
+      !(in_slack(lane) / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane))) >= -1e-9))
+    bad = 1.0;
   if (!(wmax(bad) == 0.0) || !isfinite(xs)) return;
   if (gx != nullptr && lane < NX) gx[static_cast<size_t>(env) * NX + lane] = xi;
   if (lane >= NV && lane < NV + NU) gtau[static_cast<size_t>(env) * NU + lane - NV] = xi;

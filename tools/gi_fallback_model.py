@@ -1,7 +1,7 @@
 """Numpy model of the wheel-row fallback kernel (osc_batch.hip, osc_gi_kernel): Goldfarb & Idnani's
 dual active-set method on the FULL QP of one env (x = (dv, u, z), the reference's rows) for the
 envs the interior point leaves at max_iter.  The same algorithm and update order as the kernel --
-J = L^-T Q and R kept by Givens rotations, equality rows first (never dropped), then the most
+J = L^-T Q and R kept by Givens rotations (an added row's from suffix norms of d), equality rows first (never dropped), then the most
 violated one-sided row -- so its iterates can be compared step by step.  Not product code.
 
     python tools/gi_fallback_model.py SEED_OFFSET CENSUS_JSONL     (MAX_ITER envs of a census)
@@ -59,12 +59,19 @@ def gi_full(H, f, cs, bs, eqs, max_steps=400):
     jscale = np.linalg.norm(Jm, axis=1).max()
 
     def add(d, q):
+        # the rotations (j-1, j), j = n-1 .. q+1, that fold d[q+1:] into d[q]: rotation j meets
+        # (d[j-1], ||d[j:]||) (d[n-1] itself, signed, for the first), so its (c, s) follow from the
+        # suffix sums of squares -- all at once, no chain (the kernel: one wave scan)
         nonlocal Jm
-        for j in range(n - 1, q, -1):
-            c, s, r = givens(d[j - 1], d[j])
-            d[j - 1], d[j] = r, 0.0
-            a, b = Jm[:, j - 1].copy(), Jm[:, j].copy()
-            Jm[:, j - 1], Jm[:, j] = c * a + s * b, -s * a + c * b
+        if q < n - 1:
+            S = np.cumsum((d[q:] ** 2)[::-1])[::-1]          # S[j - q] = sum_{k >= j} d_k^2
+            for j in range(n - 1, q, -1):
+                rr = np.sqrt(S[j - 1 - q])
+                c, s = (1.0, 0.0) if rr == 0.0 else (
+                    d[j - 1] / rr, (d[j] if j == n - 1 else np.sqrt(S[j - q])) / rr)
+                a, b = Jm[:, j - 1].copy(), Jm[:, j].copy()
+                Jm[:, j - 1], Jm[:, j] = c * a + s * b, -s * a + c * b
+            d[q] = np.sqrt(S[0])
         R[:q + 1, q] = d[:q + 1]
 
     def drop(k, q):
