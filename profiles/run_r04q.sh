@@ -19,4 +19,7 @@ timeout -k 10 200 python bench.py --robot walter_sr --scenario tumbling --mask b
 timeout -k 10 200 python bench.py --nenv-per-gpu 8192 $B > $O/bench_go2_8192.json 2>> $O/err.txt || exit 15
 timeout -k 10 200 python bench.py --nenv-per-gpu 65536 --no-cpu --no-front-end --no-single-env --no-north-star --no-mixed > $O/bench_go2_65536.json 2>> $O/err.txt || exit 16
 timeout -k 10 200 python bench.py --robot mixed --no-cpu --no-warm --no-front-end --no-single-env --no-north-star > $O/bench_mixed.json 2>> $O/err.txt || exit 17
+timeout -k 10 200 python tools/wheel_census.py 2048 93 tumbling bernoulli 1 {} --dump=$O/dump_93.npz > $O/dump_93.jsonl 2>&1 || exit 18
+timeout -k 10 300 python tools/wheel_census.py 2048 97 tumbling bernoulli 5 {} --dump=$O/dump_97.npz > $O/dump_97.jsonl 2>&1 || exit 19
+OSC_LIB_PATH=operational-space-control_amd/lib/ab/giprof/libosc_batch.so timeout -k 10 200 python tools/wheel_census.py 2048 86 tumbling bernoulli 1 {} --brief > $O/giprof_86.txt 2>&1 || exit 20
 echo done

@@ -4,7 +4,8 @@ not reported OK (or OK but not certified) their status, iterations and torque er
 exact oracle.  One parameterised tool in place of round 3's wheel_* one-offs.
 
     python tools/wheel_census.py [nenv] [seed] [scenario] [mask] [warm_ticks] [tuning-json] [--brief]
-(--brief: the per-tick summary lines only, no oracle solves)
+(--brief: the per-tick summary lines only, no oracle solves; --dump=OUT.npz: x, y, status and the
+inputs of every env not certified, for a CPU look at its certificate)
 """
 import json
 import os
@@ -31,7 +32,9 @@ YAML = os.path.join(os.path.dirname(config_path("walter_sr_wheels")),
 
 def main():
     brief = "--brief" in sys.argv
-    sys.argv = [a for a in sys.argv if a != "--brief"]
+    dump = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--dump=")), None)
+    sys.argv = [a for a in sys.argv if a != "--brief" and not a.startswith("--dump=")]
+    dumps = {}
     nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     seed = SEED_BASE + (int(sys.argv[2]) if len(sys.argv) > 2 else 86)
     scenario = sys.argv[3] if len(sys.argv) > 3 else "tumbling"
@@ -82,6 +85,14 @@ def main():
         print(json.dumps(row), flush=True)
         tau = out.tau.cpu().numpy()
         it = out.iters.cpu().numpy()
+        if dump:
+            for e in np.nonzero(~good)[0]:
+                key = f"t{tick}_e{e}"
+                dumps[key + "_x"] = out.x[e].cpu().numpy()
+                dumps[key + "_y"] = out.y[e].cpu().numpy()
+                dumps[key + "_wd"] = wd[e]
+                for k in ("M", "C", "J", "b", "T", "mask"):
+                    dumps[f"{key}_{k}"] = np.asarray(d[k][e])
         for e in [] if brief else np.nonzero((st != 0) | ~good)[0][:24]:
             a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
             ref = torque(model, solve_exact(model, build_qp(model, *a, wheel, wd[e]), *a[:3]).x)
@@ -91,6 +102,8 @@ def main():
                               "cert": {k: float(v[e].item()) for k, v in cert.items()},
                               "ncontact": int(d["mask"][e].sum())}), flush=True)
         d = random_walk(d, rng)
+    if dump:
+        np.savez(dump, **dumps)
 
 
 if __name__ == "__main__":
