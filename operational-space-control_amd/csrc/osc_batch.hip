@@ -3258,6 +3258,13 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   }
 }
 
+// a wave-uniform lane's double (v_readlane_b32 x2: no LDS round trip)
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 // ==================== kernel 4: wheel-row fallback (Goldfarb-Idnani, optional) ==================
 // An env the wheel-row interior point leaves at max_iter (~0.5 % of tumbling envs: QPs whose
 // multipliers reach 1e7-3e8 -- the rows nearly inconsistent with the torque limits, DESIGN.md
@@ -3297,7 +3304,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   __shared__ double sEb[NEQ];
   __shared__ double sJ[NX * NXP];             // J (row i at i * NXP); first the Cholesky factor
   __shared__ double sR[NX * NXP];             // R, upper triangular (row i at i * NXP)
-  __shared__ double sx[NX], sc[NX], sd[NX], sgc[NX], sgs[NX];
+  __shared__ double sx[NX], sc[NX], sd[NX], sgc[NX], sgs[NX], sRi[NX];   // sRi: 1 / R[j][j]
   const double* wenv = ws + static_cast<size_t>(env) * D::WS;
   const double* M = gM + static_cast<size_t>(env) * NV * NV;
   const double* C = gC + static_cast<size_t>(env) * NV;
@@ -3504,7 +3511,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     double dv = lane < q ? sd[lane] : 0.0;
     rj = 0.0;
     for (int jj = q - 1; jj >= 0; --jj) {   // back substitution, column-oriented
-      const double v = __shfl(dv, jj, kWave) / sR[jj * NXP + jj];
+      const double v = readlane_d(dv, jj) * sRi[jj];
       if (lane == jj) rj = v;
       if (lane < jj) dv = fma(-sR[lane * NXP + jj], v, dv);
     }
@@ -3551,7 +3558,10 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       for (int c = 0; c < NX; ++c) sJ[lane * NXP + c] = row[c];
     }
     if (lane < q) sR[lane * NXP + q] = dl;
-    if (lane == q) sR[q * NXP + q] = dq;
+    if (lane == q) {
+      sR[q * NXP + q] = dq;
+      sRi[q] = 1.0 / dq;
+    }
     __syncthreads();
   };
   // working row k leaves: R's columns k+1.. shift left and are re-triangularised by rotations of
@@ -3582,6 +3592,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       __syncthreads();
     }
     if (lane < NX) sR[(q - 1) * NXP + lane] = 0.0;
+    if (lane >= k && lane < q - 1) sRi[lane] = 1.0 / sR[lane * NXP + lane];
     if (lane < NX) {
       for (int j = k; j < q - 1; ++j) {
         const double c = sgc[j], s = sgs[j];
@@ -3602,12 +3613,23 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
 
   bool ok = true;
   int steps = 0;
+#ifdef OSC_GI_PROFILE
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1_ = 0;
+  int ndrop = 0, nadd = 0;
+#define GI_T0() asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory")
+#define GI_T1(k) do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory"); tp[k] += t1_ - t0; } while (0)
+#else
+#define GI_T0() do {} while (0)
+#define GI_T1(k) do {} while (0)
+#endif
   // ---- equality rows: always in, never dropped; a row dependent on those already in skipped ----
   for (int k = 0; k < neq && ok; ++k) {
     const double ck = lane < NX ? sE[k * NXP + lane] : 0.0;
     if (lane < NX) sc[lane] = ck;
     __syncthreads();
+    GI_T0();
     directions(-1);
+    GI_T1(0);
     const double zmax = wmax(fabs(zi)), cmax = wmax(fabs(ck));
     if (zmax <= 1e-13 * cmax * (1.0 + jscale)) continue;
     const double cx = wsum(ck * xi), zc = wsum(zi * ck);
@@ -3616,7 +3638,9 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     xi = fma(t, zi, xi);
     if (lane < q) up = fma(-t, rj, up);
     if (lane == q) { up = t; act = k; }
+    GI_T0();
     add_row();
+    GI_T1(1);
     ++q;
   }
   if (lane < NX) sx[lane] = xi;
@@ -3624,6 +3648,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   // ---- one-sided rows ----
   while (ok) {
     if (++steps > kMaxSteps) { ok = false; break; }
+    GI_T0();
     // working one-sided rows as a bit set over p
     unsigned long long in_set = (lane < q && act >= kIneq) ? (1ull << (act - kIneq)) : 0ull;
     for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -3637,6 +3662,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     if (in_valid(lane) && !((in_set >> lane) & 1ull))
       viol = in_slack(lane) / (1.0 + in_scale(lane) * xs + fabs(in_rhs(lane)));
     wargmin(viol, p);
+    GI_T1(2);
     if (!(viol < -1e-14)) break;   // every one-sided row holds: optimal
     const double cp = lane < NX ? in_coef(p, lane) : 0.0;
     const double bp = in_rhs(p), scp = in_scale(p);
@@ -3645,7 +3671,9 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     if (lane == q) up = 0.0;
     while (true) {
       if (++steps > kMaxSteps) { ok = false; break; }
+      GI_T0();
       directions(p);
+      GI_T1(3);
       // partial step: the working one-sided row whose multiplier reaches 0 first
       const double rmax = 1.0 + wmax(lane < q ? fabs(rj) : 0.0);
       double t1 = INFINITY;
@@ -3665,14 +3693,29 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       __syncthreads();
       if (t2 <= t1) {   // full step: p joins
         if (lane == q) act = kIneq + p;
+        GI_T0();
         add_row();
+        GI_T1(4);
+#ifdef OSC_GI_PROFILE
+        ++nadd;
+#endif
         ++q;
         break;
       }
+      GI_T0();
       drop_row(kd);
+      GI_T1(5);
+#ifdef OSC_GI_PROFILE
+      ++ndrop;
+#endif
       --q;
     }
   }
+#ifdef OSC_GI_PROFILE
+  if (lane == 0)
+    printf("gi env %d ok %d steps %d neq %d q %d adds %d drops %d cyc eqdir %llu eqadd %llu scan %llu dir %llu add %llu drop %llu\n",
+           env, ok ? 1 : 0, steps, neq, q, nadd, ndrop, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]);
+#endif
   if (!ok) return;
   // ---- certify: every equality row held, every one-sided row feasible ----
   const double xs = wmax(lane < NX ? fabs(xi) : 0.0);

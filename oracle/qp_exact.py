@@ -138,8 +138,11 @@ def kkt_certificate(qp: QPData, x: np.ndarray, y: np.ndarray) -> dict:
     dual_inf = max(np.where(hi_fin, 0.0, yp).max(), np.where(lo_fin, 0.0, ym).max())
     one_sided = qp.l != qp.u
     scale_y = 1.0 + (np.abs(y[one_sided]).max() if one_sided.any() else 0.0)
-    gap_hi = np.where(hi_fin, qp.u - Ax, 0.0)
-    gap_lo = np.where(lo_fin, Ax - qp.l, 0.0)
+    # complementarity over the one-sided rows: an equality row's multiplier is free and its
+    # residual is the primal measure (nearly dependent wheel rows carry multipliers ~1e13, whose
+    # product with a 1e-9 residual is no complementarity gap)
+    gap_hi = np.where(hi_fin & one_sided, qp.u - Ax, 0.0)
+    gap_lo = np.where(lo_fin & one_sided, Ax - qp.l, 0.0)
     comp = np.maximum(np.abs(yp * gap_hi), np.abs(ym * gap_lo)).max()
     return dict(stationarity=float(np.abs(stat).max() / scale_d),
                 primal=float(viol.max() / scale_p),

@@ -4,7 +4,9 @@ difference against the first setting.  Replaces the OSC_* environment-variable s
 1-3 (the release library reads no environment).
 
     python tools/tune_ab.py ROBOT NENV SCENARIO MASK '{"eps_mu": 1e-9}' '{"eps_mu": 1e-6}' ...
-    (SCENARIO standing|tumbling|qpos<range>: joint states through the GPU kinematics)
+    (SCENARIO standing|tumbling|qpos<range>: joint states through the GPU kinematics;
+     OSC_AB_ROUNDS=R: R interleaved rounds over the settings, the median time per setting -- one
+     round's first setting also pays the clocks' ramp)
 """
 import json
 import os
@@ -37,24 +39,30 @@ def main():
     tunings = [json.loads(a) for a in sys.argv[5:]] or [{}]
     d = inputs(robot, nenv, scenario, mask_mode)
     ref = None
-    for tn in tunings:
-        s = OSCBatchSolver(robot, tuning=tn)
-        args = s.prepare(**d)
-        out = s.alloc_outputs(nenv)
-        for _ in range(5):
-            s.solve_into(out, *args)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(30):
-            s.solve_into(out, *args)
-        b.record()
-        torch.cuda.synchronize()
+    rounds = int(os.environ.get("OSC_AB_ROUNDS", "1"))
+    solvers = [OSCBatchSolver(robot, tuning=tn) for tn in tunings]
+    argss = [s.prepare(**d) for s in solvers]
+    outs = [s.alloc_outputs(nenv) for s in solvers]
+    times = [[] for _ in tunings]
+    for _ in range(rounds):
+        for k, s in enumerate(solvers):
+            for _ in range(5):
+                s.solve_into(outs[k], *argss[k])
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(30):
+                s.solve_into(outs[k], *argss[k])
+            b.record()
+            torch.cuda.synchronize()
+            times[k].append(a.elapsed_time(b) / 30)
+    for k, tn in enumerate(tunings):
+        s, out = solvers[k], outs[k]
         tau = out.tau.cpu().numpy()
         st = out.status.cpu().numpy()
         it = out.iters.cpu().numpy()
         row = {"robot": robot, "nenv": nenv, "scenario": scenario, "tuning": tn,
-               "ms": round(a.elapsed_time(b) / 30, 4),
+               "ms": round(float(np.median(times[k])), 4), "ms_rounds": [round(t, 4) for t in times[k]],
                "status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
                "iters_mean": round(float(it.mean()), 3), "iters_max": int(it.max()),
                "wave_iters_mean": round(float(np.max(np.reshape(it[:nenv // 4 * 4], (-1, 4)), 1).mean()), 3)}
