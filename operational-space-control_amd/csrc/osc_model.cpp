@@ -233,6 +233,10 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   if (ns_flag == "true" || ns_flag == "True" || ns_flag == "1") {
     desc->wheel_rows = 1;
     desc->eps_mu = 1e-12;   // the wheel rows' interior point keeps the late stop (above)
+    // the active-set fallback (osc_gi_kernel) takes every env the interior point leaves at
+    // max_iter, so the cap can sit just above the converging envs' 21 iterations: 2,048 tumbling
+    // envs 5.34 -> 4.53 ms per solve, all OK and certified either way (profiles/r04w/)
+    desc->max_iter = 25;
     const auto& rl = y.lists["wheel_radius"];
     double r = 0.0;
     const bool scalar_r = rl.empty() && to_double(y.scalars["wheel_radius"], &r);
