@@ -536,17 +536,38 @@ __device__ __forceinline__ void wave_mgs(double* rows, int stride, int ncol, int
   }
 }
 
-// The same over rows held in LDS (loops not unrolled: for long row sets).
+// Gram-Schmidt over the `nrows` rows of an LDS row set (row stride `stride`, `ncol` columns, one
+// lane per column): the first `ndot` columns are made orthonormal, the other columns follow the
+// same row operations (a right-hand side, identity columns accumulating the transform).  A row
+// whose residual is not above `drop` x its original norm is dependent on the earlier ones and
+// becomes zero (with its transform row).  Every decision is wave-uniform.
+// Classical Gram-Schmidt applied twice (CGS2), not modified: the projections of row w on all
+// earlier rows come from one pass with lane v forming row v's dot product (no 64-lane reduction
+// per pair -- modified Gram-Schmidt's 1,128 dependent reductions for the 48-row basis completion
+// were most of the wheel model's setup: 975 -> 564 us for 2,048 envs), then lane c subtracts them
+// from column c; the second pass restores orthogonality to working precision.  (For the 16-row
+// sets the register-resident wave_mgs above stays: this LDS form measured 2.3x slower there,
+// profiles/r04za/.)  `scf`: nrows doubles of LDS scratch.
 __device__ __noinline__ void wave_mgs_lds(double* rows, int nrows, int stride, int ncol, int ndot,
-                                          int lane, double drop) {
+                                          int lane, double drop, double* scf) {
   const bool cv = lane < ncol, dv = lane < ndot;
   for (int w = 0; w < nrows; ++w) {
     double aw = cv ? rows[w * stride + lane] : 0.0;
     const double n0 = sqrt(wave_sum(dv ? aw * aw : 0.0));
-    for (int v = 0; v < w; ++v) {
-      const double av = cv ? rows[v * stride + lane] : 0.0;
-      const double cf = wave_sum(dv ? av * aw : 0.0);
-      aw = fma(-cf, av, aw);
+    for (int pass = 0; pass < 2 && w > 0; ++pass) {
+      double cf = 0.0;
+      if (lane < w) {
+        for (int c = 0; c < ndot; ++c) cf = fma(rows[lane * stride + c], rows[w * stride + c], cf);
+      }
+      if (lane < w) scf[lane] = cf;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (cv) {
+        for (int v = 0; v < w; ++v) aw = fma(-scf[v], rows[v * stride + lane], aw);
+        rows[w * stride + lane] = aw;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
     }
     const double nn = sqrt(wave_sum(dv ? aw * aw : 0.0));
     const double sc = (nn > drop * n0 && nn > 0.0) ? 1.0 / nn : 0.0;
@@ -1021,7 +1042,7 @@ __device__ __forceinline__ void setup_env(
       sWT[p] = (w < NW) ? sWA[w * WAST + c] : ((c == w - NW) ? 1.0 : 0.0);
     }
     wave_sync();
-    wave_mgs_lds(sWT, NW + NY, NY, NY, NY, lane, 1e-9);
+    wave_mgs_lds(sWT, NW + NY, NY, NY, NY, lane, 1e-9, sWE);   // (sWE: copied out above, free)
     wave_sync();
     int kept = 0;
     for (int w = 0; w < NW + NY; ++w) {
@@ -2968,6 +2989,20 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     if (lane < NW) chol_solve(sE + lane * NV);        // row w <- (M^-1 E')[:, w]
     if (lane == NW) chol_solve(sv0);                  // nu0 = -M^-1 g0
     __syncthreads();
+    // the contact rows of J against W's columns and nu0 (Jc_k' W, Jc_k' nu0), all lanes: the
+    // least-squares rows below are combinations of them (lane 0 formed each one serially)
+    __shared__ double sJW[3 * NC * (NW > 0 ? NW : 1)];
+    __shared__ double sJN0[3 * NC];
+    for (int p = lane; p < 3 * NC * NW + 3 * NC; p += kWave) {
+      const int kc = p < 3 * NC * NW ? p / NW : p - 3 * NC * NW;
+      const double* jr = J + (JC0 + kc) * NV;
+      const double* v = p < 3 * NC * NW ? sE + (p % NW) * NV : sv0;
+      double a = 0.0;
+      for (int i = 0; i < NV; ++i) a = fma(jr[i], v[i], a);
+      if (p < 3 * NC * NW) sJW[p] = a;
+      else sJN0[kc] = a;
+    }
+    __syncthreads();
     if (lane == 0) {
       const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg, mu = P->mu;
       int n = 0;
@@ -3032,16 +3067,10 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
           double* row = sA + n * NW;   // (built in place)
           for (int w = 0; w < NW; ++w) row[w] = 0.0;
           for (int cc = 0; cc < 3; ++cc) {
-            const double* jr = J + (JC0 + 3 * k + cc) * NV;
-            double jn0 = 0.0;
-            for (int i = 0; i < NV; ++i) jn0 = fma(jr[i], sv0[i], jn0);
+            const double jn0 = sJN0[3 * k + cc];
             const double fc = cc == 0 ? f0 : (cc == 1 ? f1 : f2);
             rhs = fma(pc[nc][cc], wz * fc - jn0, rhs);
-            for (int w = 0; w < NW; ++w) {
-              double jw = 0.0;
-              for (int i = 0; i < NV; ++i) jw = fma(jr[i], sE[w * NV + i], jw);
-              row[w] = fma(pc[nc][cc], jw, row[w]);
-            }
+            for (int w = 0; w < NW; ++w) row[w] = fma(pc[nc][cc], sJW[(3 * k + cc) * NW + w], row[w]);
           }
           sb[n++] = -rhs;   // row . nu_w = -rhs
           ++nc;
@@ -3050,58 +3079,72 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
       snrow = n;
     }
     __syncthreads();
-    if (lane == 0) {
-      // the basic least-squares solution by Householder QR with column pivoting (rank: |R_jj| >
-      // 1e-10 |R_00|; the dependent rows' multipliers are zero).  (Normal equations do not do:
-      // the rows that fix dv need multipliers up to ~1e6 along directions whose singular values
-      // are ~1e-9 of the largest -- squared, they drown in rounding.)
-      const int n = snrow;
-      double* A = sA;
-      double* bb = sb;
-      for (int c = 0; c < NW; ++c) spiv[c] = c;
-      double nmax0 = 0.0;
-      int rank = 0;
-      for (int j = 0; j < NW && j < n; ++j) {
-        int p = j;
-        double best = -1.0;
-        for (int c = j; c < NW; ++c) {
-          double v = 0.0;
-          for (int t = j; t < n; ++t) v = fma(A[t * NW + c], A[t * NW + c], v);
-          if (v > best) { best = v; p = c; }
-        }
-        const double cn = sqrt(best);
-        if (j == 0) nmax0 = cn;
-        if (!(cn > 1e-10 * nmax0) || cn == 0.0) break;
-        if (p != j) {
-          for (int t = 0; t < n; ++t) {
-            const double tmp = A[t * NW + j];
-            A[t * NW + j] = A[t * NW + p];
-            A[t * NW + p] = tmp;
-          }
-          const int ti = spiv[j]; spiv[j] = spiv[p]; spiv[p] = ti;
-        }
-        const double ajj = A[j * NW + j];
-        const double alpha = ajj > 0.0 ? -cn : cn;
-        // v = A[j:, j] - alpha e_1;  H = I - 2 v v' / (v'v)
-        const double v0 = ajj - alpha;
-        const double vn2 = 2.0 * cn * (cn + fabs(ajj));   // = v'v, cancellation-free
-        if (vn2 > 0.0) {
-          for (int c = j + 1; c < NW; ++c) {
-            double sd = v0 * A[j * NW + c];
-            for (int t = j + 1; t < n; ++t) sd = fma(A[t * NW + j], A[t * NW + c], sd);
-            const double f = 2.0 * sd / vn2;
-            A[j * NW + c] -= f * v0;
-            for (int t = j + 1; t < n; ++t) A[t * NW + c] = fma(-f, A[t * NW + j], A[t * NW + c]);
-          }
-          double sd = v0 * bb[j];
-          for (int t = j + 1; t < n; ++t) sd = fma(A[t * NW + j], bb[t], sd);
-          const double f = 2.0 * sd / vn2;
-          bb[j] -= f * v0;
-          for (int t = j + 1; t < n; ++t) bb[t] = fma(-f, A[t * NW + j], bb[t]);
-        }
-        A[j * NW + j] = alpha;
-        rank = j + 1;
+    // the basic least-squares solution by Householder QR with column pivoting (rank: |R_jj| >
+    // 1e-10 |R_00|; the dependent rows' multipliers are zero).  (Normal equations do not do: the
+    // rows that fix dv need multipliers up to ~1e6 along directions whose singular values are
+    // ~1e-9 of the largest -- squared, they drown in rounding.)  Lane c owns column c (lane NW:
+    // the right-hand side b): norms, reflections and updates run per column in parallel, each in
+    // the serial order.
+    const int n = snrow;
+    double* A = sA;
+    double* bb = sb;
+    if (lane < NW) spiv[lane] = lane;
+    double nmax0 = 0.0;
+    int rank = 0;
+    for (int j = 0; j < NW && j < n; ++j) {
+      double v = -1.0;
+      int p = lane;
+      if (lane >= j && lane < NW) {
+        v = 0.0;
+        for (int t = j; t < n; ++t) v = fma(A[t * NW + lane], A[t * NW + lane], v);
       }
+      for (int o = kWave / 2; o > 0; o >>= 1) {   // the largest, the lowest column among ties
+        const double ov = __shfl_xor(v, o, kWave);
+        const int op = __shfl_xor(p, o, kWave);
+        if (ov > v || (ov == v && op < p)) {
+          v = ov;
+          p = op;
+        }
+      }
+      const double cn = sqrt(v);
+      if (j == 0) nmax0 = cn;
+      if (!(cn > 1e-10 * nmax0) || cn == 0.0) break;
+      __syncthreads();
+      if (p != j) {   // lanes j and p swap their columns (row t: both read, then both write)
+        if (lane == j || lane == p) {
+          const int o = lane == j ? p : j;
+          for (int t = 0; t < n; ++t) {
+            const double a = A[t * NW + o];
+            A[t * NW + lane] = a;
+          }
+        }
+        if (lane == 0) {
+          const int ti = spiv[j];
+          spiv[j] = spiv[p];
+          spiv[p] = ti;
+        }
+        __syncthreads();
+      }
+      const double ajj = A[j * NW + j];
+      const double alpha = ajj > 0.0 ? -cn : cn;
+      // v = A[j:, j] - alpha e_1;  H = I - 2 v v' / (v'v)
+      const double v0 = ajj - alpha;
+      const double vn2 = 2.0 * cn * (cn + fabs(ajj));   // = v'v, cancellation-free
+      if (vn2 > 0.0 && lane > j && lane <= NW) {
+        double* col = lane < NW ? A + lane : bb;
+        const int cs = lane < NW ? NW : 1;
+        double sd = v0 * col[j * cs];
+        for (int t = j + 1; t < n; ++t) sd = fma(A[t * NW + j], col[t * cs], sd);
+        const double f = 2.0 * sd / vn2;
+        col[j * cs] -= f * v0;
+        for (int t = j + 1; t < n; ++t) col[t * cs] = fma(-f, A[t * NW + j], col[t * cs]);
+      }
+      __syncthreads();
+      if (lane == j) A[j * NW + j] = alpha;
+      rank = j + 1;
+      __syncthreads();
+    }
+    if (lane == 0) {
       for (int a = 0; a < NW; ++a) snu[a] = 0.0;
       for (int a = rank - 1; a >= 0; --a) {   // R z = Q'b, z -> nu_w[piv]
         double v = bb[a];
