@@ -1,5 +1,7 @@
 """Diagnostic: per-phase cycle shares of the IPM kernel from the OSC_STAMPS build
-(lib/libosc_batch_stamps.so).  Stamps serialise the wave, so read SHARES, not absolute time."""
+(lib/libosc_batch_stamps.so).  Stamps serialise the wave, so read SHARES, not absolute time.
+
+    python tools/stamps.py [nenv] [robot ...]     (robots: unitree_go2 walter_sr noslip)"""
 import ctypes
 import json
 import os
@@ -19,13 +21,27 @@ NAMES = ["stage+rows", "iter-head(Gy,mu,D)", "assemble: contact blocks", "LDL^T"
          "rhs (2 passes)", "solve (2 passes)", "Gdy+ratio+reduce (2 passes)", "update",
          "assemble: rd = g + G'lam + Hr y", "assemble: rank-1 U terms",
          "refine: K_A + LDL", "refine: steps"]
-for robot in ["unitree_go2", "walter_sr"]:
+for robot in (sys.argv[2:] or ["unitree_go2", "walter_sr"]):
     nenv = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
-    s = OSCBatchSolver(robot)
-    d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
+    if robot == "noslip":   # the opt-in wheel rows, 2,048-env-census shape (tumbling, Bernoulli)
+        from osc_amd.robots import config_path
+        from osc_amd.synth import WALTER_WHEEL_DOFS, WHEEL_RADIUS, wheel_directions
+        yaml = os.path.join(os.path.dirname(config_path("walter_sr_wheels")),
+                            "walter_sr_wheels_noslip_config.yaml")
+        s = OSCBatchSolver("walter_sr_wheels", yaml)
+        d = generate("walter_sr_wheels", nenv, SEED_BASE + 86, "tumbling", "bernoulli")
+        wd = torch.from_numpy(wheel_directions("walter_sr_wheels", d, WALTER_WHEEL_DOFS,
+                                               np.full(8, WHEEL_RADIUS), SEED_BASE + 87)).cuda()
+    else:
+        s = OSCBatchSolver(robot)
+        d = generate(robot, nenv, SEED_BASE + 2, "standing", "ones")
+        wd = None
     args = s.prepare(**d)
     out = s.alloc_outputs(nenv)
-    s.solve_into(out, *args)
+    if wd is None:
+        s.solve_into(out, *args)
+    else:
+        s.solve_into(out, *args, wheel_dir=wd)
     torch.cuda.synchronize()
     nblk = nenv // 4
     buf = (ctypes.c_ulonglong * (nblk * len(NAMES)))()
