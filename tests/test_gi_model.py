@@ -28,7 +28,7 @@ def test_gi_full_qp_matches_oracle(envs):
     for e in envs:
         a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a, wheel, wd[e])
-        cs, bs, eqs = rows_of(qp, model.n)
+        cs, bs, eqs = rows_of(qp, model.n, model)
         x, act, steps, ok = gi_full(qp.H, qp.f, cs, bs, eqs)
         assert ok, (e, steps)
         eq_res = max(abs(cs[k] @ x - bs[k]) / (1 + abs(bs[k])) for k in range(int(eqs.sum())))

@@ -27,22 +27,42 @@ def givens(a, b):
     return a / r, b / r, r
 
 
-def rows_of(qp, n):
-    """(normals c, rhs b, is_equality) with rows as c'x >= b (equalities c'x = b)."""
-    cs, bs, eqs = [], [], []
+def rows_of(qp, n, model=None):
+    """(normals c, rhs b, is_equality) with rows as c'x >= b (equalities c'x = b), in the kernel's
+    order: the equality rows as the QP stacks them (dynamics, wheel rows, then the forces of
+    contacts off the ground), then the one-sided rows as osc_gi_kernel numbers them -- per torque
+    (upper, lower), then per contact (4 pyramid rows, fz >= lb, fz <= ub)."""
     A, l, u = qp.A, qp.l, qp.u
+    cs, bs, eqs = [], [], []
     for i in range(A.shape[0]):
         lo, hi = l[i] > -OSQP_INFTY / 2, u[i] < OSQP_INFTY / 2
         if lo and hi and l[i] == u[i]:
             cs.append(A[i]); bs.append(u[i]); eqs.append(True)
+    one = []   # (key, c, b)
+    for i in range(A.shape[0]):
+        lo, hi = l[i] > -OSQP_INFTY / 2, u[i] < OSQP_INFTY / 2
+        if lo and hi and l[i] == u[i]:
             continue
-        if hi:
-            cs.append(-A[i]); bs.append(-u[i]); eqs.append(False)
-        if lo:
-            cs.append(A[i]); bs.append(l[i]); eqs.append(False)
-    order = sorted(range(len(cs)), key=lambda k: not eqs[k])   # equalities first
-    return ([cs[k] for k in order], np.array([bs[k] for k in order]),
-            np.array([eqs[k] for k in order]))
+        nz = np.nonzero(A[i])[0]
+        if model is not None and len(nz) == 1 and model.nv <= nz[0] < model.nv + model.nu:
+            q = nz[0] - model.nv
+            if hi: one.append(((q, 0), -A[i], -u[i]))
+            if lo: one.append(((q, 1), A[i], l[i]))
+        elif model is not None and len(nz) == 1 and nz[0] >= model.nv + model.nu:
+            k = (nz[0] - model.nv - model.nu) // 3
+            if lo: one.append(((model.nu + k, 4), A[i], l[i]))
+            if hi: one.append(((model.nu + k, 5), -A[i], -u[i]))
+        elif model is not None:
+            k = (nz[0] - model.nv - model.nu) // 3   # pyramid row of contact k, in A's order
+            r = sum(1 for key, _, _ in one if key[0] == model.nu + k and key[1] < 4)
+            one.append(((model.nu + k, r), -A[i], -u[i]))
+        else:
+            if hi: one.append(((i, 0), -A[i], -u[i]))
+            if lo: one.append(((i, 1), A[i], l[i]))
+    one.sort(key=lambda t: t[0])
+    for _, c, b in one:
+        cs.append(c); bs.append(b); eqs.append(False)
+    return cs, np.array(bs), np.array(eqs)
 
 
 def gi_full(H, f, cs, bs, eqs, max_steps=400):
@@ -156,7 +176,7 @@ def main():
     for e in envs:
         a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
         qp = build_qp(model, *a, wheel, wd[e])
-        cs, bs, eqs = rows_of(qp, model.n)
+        cs, bs, eqs = rows_of(qp, model.n, model)
         x, act, steps, ok = gi_full(qp.H, qp.f, cs, bs, eqs)
         ref = torque(model, solve_exact(model, qp, *a[:3]).x)
         err = np.abs(torque(model, x) - ref).max() / max(np.abs(ref).max(), 1.0)
