@@ -743,9 +743,9 @@ __device__ __forceinline__ void setup_env(
     i0 *= 2;
     j0 *= 2;
     double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
-#ifdef OSC_HA_UNROLL
-#pragma unroll OSC_HA_UNROLL
-#endif
+    // (fully unrolled: unrolled 4 or 8 deep it needs 100 VGPRs instead of 256 and the CU takes 11
+    // setup waves instead of 8, but the kernel is issue-bound and gets slower, 31.6 -> 34.5 us;
+    // profiles/r04y/)
     for (int r = 0; r < S; ++r) {
       const double2 x = *reinterpret_cast<const double2*>(sA + r * NAP + i0);
       const double2 y = *reinterpret_cast<const double2*>(sA + r * NAP + j0);
