@@ -1417,13 +1417,13 @@ struct RefineLds {
 };
 // Refinement modes of the IPM body: none (the interior point alone, handing its result to
 // osc_refine_kernel through W_SOL: warm-started solves past one wave per SIMD, whose fused kernel
-// spills, and models created with OSC_REFINE_STEPS=0), the refinement pass alone
+// spills, and models created with osc_model_tuning.refine_steps = 0), the refinement pass alone
 // (osc_refine_kernel), or both in one wavefront (every cold solve and the one-wave warm solve:
 // no hand-off, no second launch).
 constexpr int kRfNone = 0, kRfOnly = 1, kRfFused = 2;
 // Full-space refinement without wheel rows: rounds of active-set changes, and
 // steps per round at most (each env stops at its own convergence, at least refine_steps)
-constexpr int kRefineRounds = 4, kRefineMaxSteps = 8;
+constexpr int kRefineRounds = 8, kRefineMaxSteps = 8;
 template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();

@@ -4,7 +4,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 export TMPDIR=/tmp
-O=gpurun_out/r04_status
+O=gpurun_out/r04_status2
 mkdir -p $O
 for rb in unitree_go2 walter_sr; do
   for sc in "standing ones" "tumbling bernoulli" "qpos0.5 ones" "qpos1.0 bernoulli"; do
