@@ -1872,6 +1872,7 @@ __device__ __forceinline__ void ipm_block(
   bool done = !valid;
   int32_t st = OSC_SOLVE_MAX_ITER;
   int it_done = 0;
+  bool stalled = false;   // WH: stopped by the late-stall exit, not at mu <= eps_mu
 
   // One loop body for everything, so factorisation and solve code exist once (I-cache).
   // it == -1 builds the initial point (Mehrotra-style):
@@ -2240,6 +2241,7 @@ __device__ __forceinline__ void ipm_block(
             done = true;
             st = OSC_SOLVE_OK;
             it_done = it;
+            stalled = true;
           }
         }
       }
@@ -2743,8 +2745,11 @@ __device__ __forceinline__ void ipm_block(
       // to ytol its iterate stands as the solution -- census, profiles/r04g_census_*: every such
       // env within 4e-12 of the exact optimum, while the refinement, started from it, ended with
       // rows violated after its rounds; the exported duals come from stationarity, not from the
-      // refinement, osc_dual_kernel)
-      if (mine && !keep && st == OSC_SOLVE_OK && !(WHR && rwmax <= ytol)) st = OSC_SOLVE_UNREFINED;
+      // refinement, osc_dual_kernel) -- but not an iterate the late-stall exit left at mu > eps_mu:
+      // with 4 refinement steps per round one such env stood 3e-4 off (profiles/r04zd/); it is
+      // UNREFINED, and the fused entries' active-set fallback solves it)
+      if (mine && !keep && st == OSC_SOLVE_OK && !(WHR && rwmax <= ytol && !stalled))
+        st = OSC_SOLVE_UNREFINED;
 #ifdef OSC_REFINE_DIAG   // diagnostic builds only: why the refinement was rejected
       if (mine && !keep)
         st = OSC_SOLVE_UNREFINED + 16 * (viol_env ? 1 : 0) + 32 * (row_min(ok) == 1.0 ? 0 : 1) +
