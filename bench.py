@@ -431,8 +431,8 @@ class DeviceClock:
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--robot", default="unitree_go2")
     ap.add_argument("--nenv-per-gpu", type=int, default=4096)
     ap.add_argument("--scenario", default="standing", choices=["standing", "tumbling"])
