@@ -275,7 +275,10 @@ int osc_dual_rows(const osc_model* model, int32_t* rows);
 
 /* osc_batch_solve with the per-call extras (NULL extras = osc_batch_solve).  A model with wheel
  * rows is solved through this entry, osc_batch_solve_warm_ex, or osc_batch_assemble_ex followed
- * by osc_batch_solve_assembled(_warm); its multi-model path returns OSC_ERR_UNSUPPORTED_DIMS. */
+ * by osc_batch_solve_assembled(_warm); its multi-model path returns OSC_ERR_UNSUPPORTED_DIMS.
+ * With wheel rows, this entry and osc_batch_solve_warm_ex re-solve every env the interior point
+ * did not leave OK by a dual active-set method on the full QP; the split entries
+ * cannot (no raw inputs) and report such an env OSC_SOLVE_MAX_ITER or OSC_SOLVE_UNREFINED. */
 int osc_batch_solve_ex(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask, const osc_solve_extras* extras,
