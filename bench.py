@@ -466,6 +466,13 @@ def parse_args(argv=None):
     ap.add_argument("--mixed-envs", type=int, default=4096,
                     help="per-model envs per GPU of the mixed (configs[4]) object")
     ap.add_argument("--no-mixed", action="store_true")
+    ap.add_argument("--hbm-batches", type=int, default=10,
+                    help="roofline.hbm_inputs: rotate this many copies of the batch (> 256 MB of "
+                         "inputs: past the Infinity Cache); 0 = off")
+    ap.add_argument("--hbm-only", action="store_true",
+                    help="run only the HBM-input rotation (for rocprofv3 --pmc passes)")
+    ap.add_argument("--hbm-traffic-json",
+                    default=os.path.join(REPO, "profiles", "pmc_traffic_hbm.json"))
     return ap.parse_args(argv)
 
 
@@ -599,7 +606,8 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
                                        f"full-space refinement runs inside it)",
                      "bytes_per_solve": bps,
                      "inputs": "cache-warm: the same batch every step (its 31 MB stays in the "
-                               "256 MB Infinity Cache); the kernel is latency-bound",
+                               "256 MB Infinity Cache); the kernel is latency-bound; "
+                               "hbm_inputs: the same QPs rotated through > 256 MB of buffers",
                      "solve_pair": {"kernel": f"osc_setup_kernel + {ipm_name}",
                                     "kernel_ms": kernel_ms, "achieved": achieved_pair,
                                     "frac": achieved_pair / HBM_PEAK_GBS,
@@ -613,6 +621,65 @@ def run_headline(args, world: int, rank: int, dev: torch.device, barrier, solver
         "converged_frac": stats.converged,
     }
     return line, solver, inputs
+
+
+def hbm_inputs(args, solver, inputs, clock, traffic_json: str) -> dict:
+    """roofline.hbm_inputs: the headline's step over inputs that come from HBM.
+    The headline solves the same 31 MB batch every step, which stays in the 256 MB Infinity Cache
+    (MALL).  Here `--hbm-batches` copies of that batch -- the same QPs, each copy's envs rotated
+    by a different offset, in their own buffers (10 x 31.4 MB = 314 MB > 256 MB) -- are solved in
+    turn, so every step's setup kernel reads inputs the previous steps have evicted.  Same QPs, so
+    the iteration counts (and the interior point's work) equal the headline's: the difference is
+    where the inputs come from.  Kernel times by HIP events as in the headline."""
+    nb = args.hbm_batches
+    nenv = inputs[0].shape[0]
+    batches = [tuple(t.roll(shifts=(i * 1031) % nenv, dims=0).contiguous() for t in inputs)
+               for i in range(nb)]
+    out = solver.alloc_outputs(nenv)
+    stream = clock.stream()
+    steps = max(args.steps, 3 * nb)
+    for k in range(max(args.warmup, nb)):
+        solver.solve_into(out, *batches[k % nb])
+    every = max(1, args.event_every)
+    sampled = [k for k in range(steps) if k % every == every - 1] or [steps - 1]
+    ev = {k: [clock.event() for _ in range(3)] for k in sampled}
+    clock.sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        inp = batches[k % nb]
+        e = ev.get(k)
+        if e:
+            e[0].record(stream)
+        solver.assemble_into(out, *inp[:5], inp[5])
+        if e:
+            e[1].record(stream)
+        solver.solve_assembled_into(out, inp[5])
+        if e:
+            e[2].record(stream)
+    clock.sync()
+    elapsed = time.perf_counter() - t0
+    setup_ms = sum(e[0].elapsed_time(e[1]) for e in ev.values()) / len(ev)
+    ipm_ms = sum(e[1].elapsed_time(e[2]) for e in ev.values()) / len(ev)
+    bps = bytes_per_solve(args.robot)
+    res = {"inputs": "hbm", "batches": nb,
+           "input_bytes_resident": int(sum(t.numel() * t.element_size() for b in batches for t in b)),
+           "steps": steps, "value": nenv * steps / elapsed, "unit": "solves/s",
+           "ms_per_step": elapsed / steps * 1e3,
+           "kernel": "osc_ipm_kernel", "kernel_ms": ipm_ms,
+           "achieved": bps * nenv / (ipm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit_bw": "GB/s",
+           "frac": bps * nenv / (ipm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "solve_pair": {"kernel_ms": setup_ms + ipm_ms,
+                          "kernel_ms_split": {"osc_setup_kernel": setup_ms, "osc_ipm_kernel": ipm_ms},
+                          "achieved": bps * nenv / ((setup_ms + ipm_ms) * 1e-3) / 1e9,
+                          "frac": bps * nenv / ((setup_ms + ipm_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS},
+           "traffic": None, "solve_pair_traffic": None}
+    if os.path.exists(traffic_json):
+        tj = json.load(open(traffic_json))
+        if tj.get("robot") == args.robot and tj.get("nenv") == nenv and tj.get("inputs") == "hbm":
+            res["traffic"] = tj.get("per_kernel", {}).get("osc_ipm_kernel")
+            res["solve_pair_traffic"] = tj.get("bytes_per_launch")
+            res["traffic_source"] = tj.get("source")
+    return res
 
 
 def attach_multi_gpu_objects(args, world, rank, dev, barrier, solver_cls, clock, line,
@@ -700,11 +767,20 @@ def main(argv=None) -> None:
 
     from osc_amd.solver import OSCBatchSolver
     clock = DeviceClock(dev)
+    if args.hbm_only:   # (profiling aid: the rotation alone, nothing else on the GPU)
+        solver = OSCBatchSolver(args.robot)
+        d = generate(args.robot, args.nenv_per_gpu, shard_seed(rank), args.scenario, args.mask)
+        print(json.dumps(hbm_inputs(args, solver, solver.prepare(**d), clock,
+                                    args.hbm_traffic_json)), flush=True)
+        return
     line, solver, inputs = run_headline(args, world, rank, dev, barrier, OSCBatchSolver, clock)
     attach_multi_gpu_objects(args, world, rank, dev, barrier, OSCBatchSolver, clock, line)
     if line is not None:
         nenv = args.nenv_per_gpu
         stream = clock.stream()
+        if world == 1 and args.hbm_batches > 0:
+            line["roofline"]["hbm_inputs"] = hbm_inputs(args, solver, inputs, clock,
+                                                         args.hbm_traffic_json)
         if world == 1 and not args.no_warm:
             line["warm"] = warm_ticks(solver, inputs, nenv, args.steps, args.warmup,
                                       shard_seed(rank) + 7, stream)

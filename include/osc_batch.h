@@ -38,7 +38,10 @@
  *   tau    [nenv][nu]             torque command = x[nv : nv+nu]
  *   x      [nenv][nv+nu+3nc]      (nullable) full design vector (dv, u, z) = get_solution()
  *   status [nenv]                 (nullable) OSC_SOLVE_* code per environment
- *   iters  [nenv]                 (nullable) interior-point iterations used
+ *   iters  [nenv]                 (nullable) interior-point iterations used; max_iter + k when
+ *                                 the warm entries' cold fix-up pass re-solved the env (k its
+ *                                 iterations); -k when the wheel rows' active-set fallback solved
+ *                                 it in k steps (osc_batch_solve_ex / _warm_ex)
  *
  * All batch pointers passed to osc_batch_solve are DEVICE pointers (HBM-resident); `stream` is
  * a hipStream_t (NULL = default stream).  The call is asynchronous with respect to the host.
@@ -55,7 +58,7 @@
 extern "C" {
 #endif
 
-#define OSC_ABI_VERSION 3
+#define OSC_ABI_VERSION 4
 #define OSC_MAX_SITES 32
 #define OSC_MAX_NU 16
 
@@ -79,9 +82,12 @@ typedef enum {
                                      refinement found no KKT point within its rounds (or was
                                      forced off by osc_model_tuning.refine_max_move): the
                                      interior point's iterate is returned, accurate only to its
-                                     stop (up to ~2e-2 normwise at eps_mu 1e-9
-                                     along the internal-force directions).  Measured: none on
-                                     the synthetic and joint-state test batches since round 4   */
+                                     stop (up to ~2e-2 normwise at eps_mu 1e-6
+                                     along the internal-force directions).  Cold entries return
+                                     it as is; the warm entries re-solve such an env cold to
+                                     mu <= 1e-12 first (then it is within ~1e-5 even if this
+                                     status remains).  Measured: none on the synthetic and
+                                     joint-state test batches since round 4                    */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C
@@ -135,9 +141,10 @@ int osc_model_create(const osc_model_desc* desc, osc_model** out);
  * bits of the result), or which kernel variant runs.  For experiments and tests. */
 typedef struct {
   int32_t refine_steps;           /* full-space refinement: minimum steps per round (each env
-                                     stops at its own convergence, at most 8); 0 = no
-                                     refinement, the interior point then runs to eps_mu <= 1e-12.
-                                     Default 2 (wheel rows: 12, fixed)                           */
+                                     stops at its own convergence, at most 8 -- a larger value is
+                                     clamped to 8); 0 = no refinement, the interior point then
+                                     runs to eps_mu <= 1e-12.  Default 2 (wheel rows: 12, fixed,
+                                     not clamped)                                                */
   double refine_max_move;         /* reject a refinement that moves y by more than this x
                                      (1 + |y|) (OSC_SOLVE_UNREFINED).  Default 1e300 (none: a
                                      kept refinement is a KKT point, i.e. the optimum)           */
@@ -249,14 +256,17 @@ typedef struct {
   int32_t* iters;                 /* nullable */
   void* workspace;
   size_t workspace_bytes;
+  const double* wheel_dir;        /* (ABI 4) [nenv][nc][6] DEVICE; required iff the model has wheel
+                                     rows (osc_solve_extras.wheel_dir), else ignored            */
 } osc_batch_job;
 
 /* Several robots' batches on one GPU in one call (BASELINE configs[4]: Go2 + WaLTER Sr shards
- * per GPU).  Results are bitwise those of one osc_batch_solve per job.  Two jobs of different
- * kernels (unitree_go2 + walter_sr) whose batches each fit one wavefront per SIMD run as ONE
- * assembly grid and ONE interior-point grid, the slower model's wavefronts first, so the other
- * model's wavefronts fill the SIMDs freed by the first one's iteration-count tail; anything else
- * runs the jobs one after another on `stream`. */
+ * per GPU).  Results are bitwise those of one osc_batch_solve (wheel rows: osc_batch_solve_ex)
+ * per job.  Two jobs of different kernels (unitree_go2 + walter_sr) whose batches each fit one
+ * wavefront per SIMD run as ONE assembly grid and ONE interior-point grid, the slower model's
+ * wavefronts first, so the other model's wavefronts fill the SIMDs freed by the first one's
+ * iteration-count tail; anything else (a wheel-row model among them) runs the jobs one after
+ * another on `stream`. */
 int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, void* stream);
 
 /* Per-call extras of osc_batch_solve_ex. */
@@ -274,11 +284,12 @@ typedef struct {
 int osc_dual_rows(const osc_model* model, int32_t* rows);
 
 /* osc_batch_solve with the per-call extras (NULL extras = osc_batch_solve).  A model with wheel
- * rows is solved through this entry, osc_batch_solve_warm_ex, or osc_batch_assemble_ex followed
- * by osc_batch_solve_assembled(_warm); its multi-model path returns OSC_ERR_UNSUPPORTED_DIMS.
- * With wheel rows, this entry and osc_batch_solve_warm_ex re-solve every env the interior point
- * did not leave OK by a dual active-set method on the full QP; the split entries
- * cannot (no raw inputs) and report such an env OSC_SOLVE_MAX_ITER or OSC_SOLVE_UNREFINED. */
+ * rows is solved through this entry, osc_batch_solve_warm_ex, osc_batch_solve_multi (its
+ * wheel_dir), or osc_batch_assemble_ex followed by osc_batch_solve_assembled(_warm).  With wheel
+ * rows every one of them re-solves each env the interior point did not leave OK by a dual
+ * active-set method on the full QP (iters = -steps, and a warm state of such an
+ * env is invalidated, so its next tick starts cold): the assembly leaves the raw rows it needs in
+ * the workspace, so the split entries run it too. */
 int osc_batch_solve_ex(const osc_model* model, int32_t nenv,
                        const double* M, const double* C, const double* J, const double* b,
                        const double* T, const double* contact_mask, const osc_solve_extras* extras,

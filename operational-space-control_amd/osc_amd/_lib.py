@@ -91,7 +91,7 @@ class OscBatchJob(ctypes.Structure):
     _fields_ = [("model", ctypes.c_void_p), ("nenv", ctypes.c_int32)] + \
         [(n, ctypes.c_void_p) for n in ("M", "C", "J", "b", "T", "contact_mask", "tau", "x",
                                          "status", "iters", "workspace")] + \
-        [("workspace_bytes", ctypes.c_size_t)]
+        [("workspace_bytes", ctypes.c_size_t), ("wheel_dir", ctypes.c_void_p)]
 
 
 _B, _S = OSC_KIN_MAX_BODIES, OSC_KIN_MAX_SITES

@@ -1,13 +1,18 @@
 """Build the in-tree native libraries: libosc_batch.so (HIP kernels for gfx950 + C-ABI + YAML
-loader) and libosc_controller.so (the OperationalSpaceController shim over the C-ABI).
+loader + kinematics + producers) and libosc_controller.so (the OperationalSpaceController shim
+over the C-ABI).
 
-    python -m osc_amd.build          (from operational-space-control_amd/)
+    python -m osc_amd.build [-f] [-v]            (from operational-space-control_amd/)
+    python -m osc_amd.build -f --out DIR -DFLAG  (a variant library for A/B timing or stamps)
 
-Plain hipcc, no cmake: five translation units.  The .so files land in
-operational-space-control_amd/lib/ so that it travels to the GPU box with the repo snapshot.
+Plain hipcc, no cmake: every translation unit compiles to its own object, in parallel (the
+interior-point kernel is instantiated in one unit per robot model for that reason), then one
+link.  The .so files land in operational-space-control_amd/lib/ so that they travel to the GPU
+box with the repo snapshot.
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
 import os
 import subprocess
 import sys
@@ -20,30 +25,65 @@ OUT_CTRL = os.path.join(PKG_DIR, "lib", "libosc_controller.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["osc_batch.hip", "osc_model.cpp", "osc_mjcf.cpp", "osc_producers.hip",
-           "osc_kinematics.hip"]
+# kernel units (csrc/osc_device.hpp lists what each holds) + host units
+SOURCES = ["osc_ipm_go2.hip", "osc_ipm_walter.hip", "osc_ipm_wheels.hip", "osc_multi.hip",
+           "osc_setup.hip", "osc_gi.hip", "osc_dual.hip", "osc_kinematics.hip",
+           "osc_producers.hip", "osc_api.hip", "osc_model.cpp", "osc_mjcf.cpp"]
+HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp"]
+# device-code units, for the static checks that read the generated assembly
+DEVICE_SOURCES = [s for s in SOURCES if s.endswith(".hip")]
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def _jobs() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:   # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def compile_flags(defines=()) -> list:
+    return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
+            "-I", os.path.join(REPO, "include"), *defines]
+
+
+def build(verbose: bool = False, force: bool = False, out: str | None = None,
+          defines=()) -> str:
+    out = out or OUT
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    hdrs = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h", "osc_kinematics.h")]
-    if not force and os.path.exists(OUT):
-        t_out = os.path.getmtime(OUT)
-        if all(os.path.getmtime(p) <= t_out for p in srcs + hdrs + [__file__]):
-            build_controller()
-            build_tick_latency()
-            return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC, "-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", "-I", os.path.join(REPO, "include"),
-           *srcs, "-o", OUT]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h",
+                                                     "osc_kinematics.h")] + [__file__]
+    variant = out != OUT
+    if not force and os.path.exists(out):
+        t_out = os.path.getmtime(out)
+        if all(os.path.getmtime(p) <= t_out for p in deps):
+            if not variant:
+                build_controller()
+                build_tick_latency()
+            return out
+    objdir = os.path.join(os.path.dirname(out), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = compile_flags(defines)
     if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    build_controller(force=True)
-    build_tick_latency(force=True)
-    return OUT
+        flags.append("-Rpass-analysis=kernel-resource-usage")
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *flags, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=_jobs()) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out],
+                   check=True)
+    if not variant:
+        build_controller(force=True)
+        build_tick_latency(force=True)
+    return out
 
 
 OUT_TICK = os.path.join(PKG_DIR, "bin", "osc_tick_latency")
@@ -79,5 +119,16 @@ def build_controller(force: bool = False) -> str:
     return OUT_CTRL
 
 
+def main(argv) -> None:
+    out, defines = None, []
+    it = iter(argv)
+    for a in it:
+        if a == "--out":
+            out = os.path.join(next(it), "libosc_batch.so")
+        elif a.startswith("-D"):
+            defines.append(a)
+    print(build(verbose="-v" in argv, force="-f" in argv, out=out, defines=defines))
+
+
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))
+    main(sys.argv[1:])

@@ -249,11 +249,14 @@ class OSCBatchSolver:
 def solve_multi_into(jobs, stream=None) -> None:
     """osc_batch_solve_multi: several models' batches in one call on one stream (BASELINE
     configs[4]: Go2 + WaLTER Sr per GPU).  `jobs` = [(solver, SolveResult, (M, C, J, b, T,
-    mask)), ...] with device tensors from solver.prepare / solver.alloc_outputs."""
+    mask)[, wheel_dir]), ...] with device tensors from solver.prepare / solver.alloc_outputs
+    (wheel_dir: the wheel-row models' directions, [nenv, nc, 6])."""
     arr = (_lib.OscBatchJob * len(jobs))()
     ptr = lambda t: t.data_ptr() if t is not None else None
     dev = None
-    for j, (solver, out, inputs) in zip(arr, jobs):
+    for j, job in zip(arr, jobs):
+        solver, out, inputs = job[:3]
+        j.wheel_dir = ptr(job[3]) if len(job) > 3 else None
         M, C, J, b, T, mask = inputs
         j.model = solver._h.value
         j.nenv = out.tau.shape[0]

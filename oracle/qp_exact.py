@@ -436,7 +436,12 @@ def solve_exact(model: OSCModel, qp: QPData, M, C, J, max_iter: int = 500,
             if method == "primal":
                 raise
     W, it = _dual_active_set(qp, eq, ineq)
-    return _finish(model, qp, eq, ineq, W, it, refine_steps)
+    sol = _finish(model, qp, eq, ineq, W, it, refine_steps)
+    # the fallback is held to the same certificate: an "exact" answer the KKT test refuses is an
+    # error, never a silent return (a GPU fallback of the same algorithm would share its faults)
+    if method == "auto" and not certified(sol.cert, 1e-8):
+        raise RuntimeError(f"dual active set ended uncertified: {sol.cert}")
+    return sol
 
 
 def certified(cert: dict, tol: float = 1e-9) -> bool:

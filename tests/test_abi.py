@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.osc_abi_version() == 3
+    assert L.osc_abi_version() == 4
     assert L.osc_status_string(2) == b"OSC_ERR_UNSUPPORTED_DIMS"
 
 

@@ -117,6 +117,27 @@ def test_split_stages_equal_fused_solve(gpu):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
 
 
+def test_refine_steps_above_round_length_clamped(gpu):
+    """without wheel rows a refinement round runs at most 8 steps, and an env counts as
+    converged only from its refine_steps-th step on, so a tuning of refine_steps = 12 used to
+    leave EVERY env UNREFINED.  osc_model_create_tuned clamps it to 8: every env OK, bitwise the
+    refine_steps = 8 solve."""
+    from osc_amd.solver import OSCBatchSolver
+    inp = generate("unitree_go2", 512, SEED_BASE + 34, "tumbling", "bernoulli")
+    outs = []
+    for steps in (12, 8):
+        s = OSCBatchSolver("unitree_go2", tuning={"refine_steps": steps})
+        args = s.prepare(**inp)
+        o = s.alloc_outputs(512, want_x=True)
+        s.solve_into(o, *args)
+        torch.cuda.synchronize()
+        outs.append(o)
+    st = outs[0].status.cpu().numpy()
+    assert (st == 0).all(), np.bincount(st)
+    for k in ("tau", "x", "status", "iters"):
+        assert torch.equal(getattr(outs[0], k), getattr(outs[1], k)), k
+
+
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
 def test_ipm_variants_bitwise_equal(gpu, robot):
     """The one-wave-per-SIMD variant (Hr in LDS where it fits, AGPR spill space) and the

@@ -275,3 +275,42 @@ def test_dual_active_set_takes_degenerate_wheel_envs():
         sol = solve_exact(model, qp, *args[:3])
         assert certified(sol.cert), (e, sol.cert)
         assert np.abs(qp.Aw @ sol.x - qp.bw).max() <= 1e-9 * (1 + np.abs(qp.bw).max())
+
+
+def test_parallel_pool_equals_serial_oracle():
+    """oracle/parallel.solve_batch (the process pool the GPU parity tests use to check every env
+    of a 4,096-env batch) returns bitwise the serial oracle's optimum, env by env, in env order."""
+    from osc_amd.synth import generate
+    from parallel import solve_batch
+    model = load_model("unitree_go2")
+    d = generate("unitree_go2", 70, 4242, "tumbling", "bernoulli")
+    xs, cert = solve_batch("unitree_go2", d["M"], d["C"], d["J"], d["b"], d["T"], d["mask"],
+                           envs=np.arange(3, 70), workers=2)
+    assert xs.shape == (67, model.n) and (cert <= 1e-8).all()
+    for e in (3, 40, 66, 69):
+        a = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
+        ref = solve_exact(model, build_qp(model, *a), *a[:3]).x
+        assert np.array_equal(xs[e - 3], ref)
+
+
+def test_seeded_oracle_equals_full_oracle():
+    """oracle/parallel.seeded_batch (every env of a 65,536-env batch against the exact optimum,
+    the working set seeded from the GPU's duals and certified by the oracle's KKT test) returns
+    the full oracle's optimum: seeded with the exact duals every env certifies and agrees to 1e-12;
+    seeded with nothing (y = 0) the certificate refuses the unconstrained face wherever a row is
+    active, and the full oracle answers."""
+    from osc_amd.synth import generate
+    from parallel import seeded_batch
+    model = load_model("unitree_go2")
+    d = generate("unitree_go2", 24, 4343, "tumbling", "bernoulli")
+    a = [d[k] for k in ("M", "C", "J", "b", "T", "mask")]
+    ref = [solve_exact(model, build_qp(model, *[v[e] for v in a]), *[v[e] for v in a[:3]])
+           for e in range(24)]
+    y = np.array([r.y for r in ref])
+    xs, seeded = seeded_batch("unitree_go2", *a, y, workers=2)
+    assert seeded.all()
+    xr = np.array([r.x for r in ref])
+    assert np.abs(xs - xr).max() <= 1e-12 * max(1.0, np.abs(xr).max())
+    xs0, seeded0 = seeded_batch("unitree_go2", *a, np.zeros_like(y), workers=2)
+    assert not seeded0.any()
+    assert np.array_equal(xs0, xr)

@@ -4,12 +4,8 @@
 #   bash tools/ab_build.sh name "-DFLAG=1 ..." [name2 "flags2" ...]
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
-C=$R/operational-space-control_amd/csrc
+cd $R/operational-space-control_amd
 while [ $# -ge 2 ]; do
   n=$1; f=$2; shift 2
-  mkdir -p $R/operational-space-control_amd/lib/ablate/$n
-  /opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -fPIC -shared $f -I $R/include \
-    $C/osc_batch.hip $C/osc_model.cpp $C/osc_mjcf.cpp $C/osc_producers.hip $C/osc_kinematics.hip \
-    -o $R/operational-space-control_amd/lib/ablate/$n/libosc_batch.so 2>&1 | grep -E "error" || true &
+  python -m osc_amd.build -f --out $R/operational-space-control_amd/lib/ablate/$n $f
 done
-wait

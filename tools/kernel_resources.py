@@ -1,7 +1,7 @@
 """Per-kernel register / scratch / occupancy table of a HIP source, from the compiler's
 kernel-resource-usage remarks (no GPU needed).
 
-    python tools/kernel_resources.py [operational-space-control_amd/csrc/osc_batch.hip] [-D...]
+    python tools/kernel_resources.py [operational-space-control_amd/csrc/osc_ipm_go2.hip] [-D...]
 """
 from __future__ import annotations
 
@@ -22,7 +22,7 @@ def demangle(names):
 
 def main(argv):
     src = next((a for a in argv[1:] if not a.startswith("-")),
-               os.path.join(REPO, "operational-space-control_amd", "csrc", "osc_batch.hip"))
+               os.path.join(REPO, "operational-space-control_amd", "csrc", "osc_ipm_go2.hip"))
     defs = [a for a in argv[1:] if a.startswith("-D")]
     with tempfile.TemporaryDirectory() as td:
         r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950",

@@ -6,11 +6,9 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/operational-space-control_amd/csrc
 if [ "$1" = "build" ]; then
+  cd $R/operational-space-control_amd
   for k in 0 1 2 3 4 5; do
-    mkdir -p $R/operational-space-control_amd/lib/ablate/kin_stop$k
-    /opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -fPIC -shared -DOSC_KIN_STOP=$k \
-      -I $R/include $C/osc_batch.hip $C/osc_model.cpp $C/osc_producers.hip $C/osc_kinematics.hip \
-      -o $R/operational-space-control_amd/lib/ablate/kin_stop$k/libosc_batch.so &
+    python -m osc_amd.build -f --out $R/operational-space-control_amd/lib/ablate/kin_stop$k -DOSC_KIN_STOP=$k
   done
   wait
   exit 0

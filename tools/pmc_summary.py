@@ -14,7 +14,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "prof")
 prefix = sys.argv[2] if len(sys.argv) > 2 else "r01_go2_4096"
 nenv = int(sys.argv[3]) if len(sys.argv) > 3 else 4096   # Go2 envs per launch of the profiled run
-dst = os.path.join(REPO, "profiles")
+# "cache" (bench.py's headline: the same batch every step) or "hbm" (bench.py --hbm-only: the batch
+# rotated through > 256 MB of buffers, roofline.hbm_inputs)
+inputs = sys.argv[4] if len(sys.argv) > 4 else "cache"
+dst = os.path.join(REPO, "profiles", os.environ.get("OSC_PROFILE_SUBDIR", ""))
 
 
 def short(name):
@@ -68,11 +71,14 @@ hb = [v.get("hbm_bytes") for v in out["kernels"].values()]
 if hb and all(h is not None for h in hb):
     # pmc_traffic.json is what bench.py's default (4,096-env) line reads; other sizes beside it
     tname = "pmc_traffic.json" if nenv == 4096 else f"pmc_traffic_{nenv}.json"
-    json.dump({"robot": "unitree_go2", "nenv": nenv, "bytes_per_launch": sum(hb),
+    if inputs == "hbm":
+        tname = "pmc_traffic_hbm.json"
+    json.dump({"robot": "unitree_go2", "nenv": nenv, "inputs": inputs, "bytes_per_launch": sum(hb),
                "per_kernel": {k: v.get("hbm_bytes") for k, v in out["kernels"].items()},
                "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per kernel (gfx950 "
                              "FETCH_SIZE halving for 16 B/lane reads; 8 B/lane reads uncalibrated)",
                "algorithmic_bytes_per_launch": 7664 * nenv,
-               "source": [f"profiles/{prefix}_pmc_fetch.csv", f"profiles/{prefix}_pmc_write.csv"]},
-              open(os.path.join(dst, tname), "w"), indent=1)
+               "source": [os.path.relpath(os.path.join(dst, f"{prefix}_pmc_{k}.csv"), REPO)
+                          for k in ("fetch", "write")]},
+              open(os.path.join(REPO, "profiles", tname), "w"), indent=1)
 print(json.dumps(out, indent=1))
