@@ -248,8 +248,18 @@ enum Stage : unsigned { kAssemble = 1u, kInteriorPoint = 2u, kBoth = 3u };
 // One call's passes: assembly (launch_setup), interior point (launch_ipm), then the wheel-row
 // fallback and the duals where asked for.
 template <class D>
-void launch_t(LaunchArgs a, unsigned stages) {
-  if (stages & kAssemble) launch_setup<D>(a);
+void launch_t(LaunchArgs a, unsigned stages, const QposArgs* q) {
+  if (stages & kAssemble) {
+#ifdef OSC_FUSED_TICK
+    if constexpr (!D::WH) {
+      if (q != nullptr) {   // the fused joint-state tick (A/B builds)
+        launch_setup_qpos<D>(a, *q);
+        q = nullptr;
+      }
+    }
+#endif
+    if (q == nullptr) launch_setup<D>(a);
+  }
   if (!(stages & kInteriorPoint)) return;
   // Wheel-row models run the active-set fallback over the envs the interior point left
   // unconverged (osc_gi_kernel; every entry point: the setup kernel left the raw rows it needs in
@@ -277,15 +287,19 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
            const double* b, const double* T, const double* contact_mask, double* tau, double* x,
            int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes,
            void* stream, unsigned stages, double* warm = nullptr, const double* wdir = nullptr,
-           double* y = nullptr) {
+           double* y = nullptr, const QposArgs* q = nullptr) {
   if (!model || nenv < 0) return OSC_ERR_INVALID_ARGUMENT;
   if (nenv == 0) return OSC_OK;
   if (!on_model_device(model)) return OSC_ERR_INVALID_ARGUMENT;
   if (!contact_mask || misaligned16(contact_mask)) return OSC_ERR_INVALID_ARGUMENT;
-  if ((stages & kAssemble) && (!M || !C || !J || !b || !T || misaligned16(M) ||
-                               misaligned16(C) || misaligned16(J) || misaligned16(b) ||
-                               misaligned16(T)))
+  if (q != nullptr) {   // joint states: the kinematics runs in the assembly kernel
+    if (!q->kin || !q->qpos || !q->qvel || !T || misaligned16(T) || stages != kBoth)
+      return OSC_ERR_INVALID_ARGUMENT;
+  } else if ((stages & kAssemble) && (!M || !C || !J || !b || !T || misaligned16(M) ||
+                                      misaligned16(C) || misaligned16(J) || misaligned16(b) ||
+                                      misaligned16(T))) {
     return OSC_ERR_INVALID_ARGUMENT;   // 16-byte alignment: vectorised staging loads
+  }
   if ((stages & kInteriorPoint) && !tau) return OSC_ERR_INVALID_ARGUMENT;
   const bool wheels = model->kid == K_WALTER_WHEELS;
   if (wheels && (stages & kAssemble) && wdir == nullptr) return OSC_ERR_INVALID_ARGUMENT;
@@ -311,13 +325,13 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
                wdir, y};
   switch (model->kid) {
     case K_GO2:
-      launch_t<Go2>(a, stages);
+      launch_t<Go2>(a, stages, q);
       break;
     case K_WALTER:
-      launch_t<Walter>(a, stages);
+      launch_t<Walter>(a, stages, q);
       break;
     case K_WALTER_WHEELS:
-      launch_t<WalterW>(a, stages);
+      launch_t<WalterW>(a, stages, q);
       break;
     default:
       rc = OSC_ERR_UNSUPPORTED_DIMS;
@@ -328,6 +342,25 @@ int launch(const osc_model* model, int32_t nenv, const double* M, const double* 
 }
 
 }  // namespace
+
+#ifdef OSC_FUSED_TICK
+namespace osc {
+int solve_qpos_fused(const osc_model* model, const QposArgs& q, int32_t nenv, const double* T,
+                     const double* contact_mask, double* tau, double* x, int32_t* status,
+                     int32_t* iters, double* warm, size_t warm_bytes, void* workspace,
+                     size_t workspace_bytes, void* stream) {
+  if (model && model->kid == K_WALTER_WHEELS) return OSC_ERR_INVALID_ARGUMENT;   // (no directions)
+  if (warm != nullptr) {
+    size_t need = 0;
+    if (!model || osc_warm_state_bytes(model, nenv < 0 ? 0 : nenv, &need) != OSC_OK ||
+        warm_bytes < need)
+      return OSC_ERR_INVALID_ARGUMENT;
+  }
+  return launch(model, nenv, nullptr, nullptr, nullptr, nullptr, T, contact_mask, tau, x, status,
+                iters, workspace, workspace_bytes, stream, kBoth, warm, nullptr, nullptr, &q);
+}
+}  // namespace osc
+#endif
 
 extern "C" int osc_batch_solve(const osc_model* model, int32_t nenv, const double* M,
                                const double* C, const double* J, const double* b, const double* T,

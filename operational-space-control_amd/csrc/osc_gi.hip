@@ -26,12 +26,11 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gmask,
     const double* __restrict__ ws, double* __restrict__ gtau, double* __restrict__ gx,
     int32_t* __restrict__ gstatus, int32_t* __restrict__ giters, double* __restrict__ gwarm) {
-  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NW = D::NW, NX = D::NX,
+  constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NW = D::NW, NX = D::NX,
                 NB = D::NB, NZ = D::NZ;
   constexpr int NXP = NX | 1;                 // odd row stride (LDS banks)
   constexpr int NEQ = NV + NW + NZ;           // dynamics, wheel rows, forces of masked contacts
   constexpr int NIN = 2 * NU + 6 * NC;        // one-sided rows: u box, pyramid, fz box
-  constexpr int JC0 = 3 * (NS - NC);          // first contact translational row of J
   constexpr int kIneq = 1 << 12;              // row ids: equality k, one-sided kIneq + p
   constexpr int kMaxSteps = 400;
   static_assert(NX <= kWave && NIN <= kWave && NEQ <= kWave, "one lane per variable / row");

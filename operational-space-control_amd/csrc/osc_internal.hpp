@@ -4,6 +4,7 @@
 // from the translation unit that holds its device code: no relocatable device code here).
 #pragma once
 #include "osc_device.hpp"
+#include "osc_qpos.hpp"
 
 struct osc_model {
   osc_model_desc desc;
@@ -36,6 +37,8 @@ struct LaunchArgs {
 };
 
 template <class D> void launch_setup(const LaunchArgs& a);   // osc_setup.hip
+template <class D> void launch_setup_qpos(const LaunchArgs& a, const QposArgs& q);   // (fused tick;
+                                                        // no wheel-row model: no directions)
 template <class D> void launch_ipm(const LaunchArgs& a);     // osc_ipm_<model>.hip
 template <class D> void launch_dual(const LaunchArgs& a);    // osc_dual.hip
 template <class D> void launch_gi(const LaunchArgs& a);      // osc_gi.hip
@@ -45,6 +48,10 @@ void launch_pair_walter_go2(const osc_batch_job& w, const osc_batch_job& g, hipS
 extern template void launch_setup<Go2>(const LaunchArgs&);
 extern template void launch_setup<Walter>(const LaunchArgs&);
 extern template void launch_setup<WalterW>(const LaunchArgs&);
+#ifdef OSC_FUSED_TICK
+extern template void launch_setup_qpos<Go2>(const LaunchArgs&, const QposArgs&);
+extern template void launch_setup_qpos<Walter>(const LaunchArgs&, const QposArgs&);
+#endif
 extern template void launch_ipm<Go2>(const LaunchArgs&);
 extern template void launch_ipm<Walter>(const LaunchArgs&);
 extern template void launch_ipm<WalterW>(const LaunchArgs&);

@@ -1432,25 +1432,42 @@ __device__ __forceinline__ void ipm_block(
             if (k + 1 >= refine_steps && __ballot(mine && !conv) == 0) break;
           }
         }
-        // rows the refined point violates join the active set
-        double nviol = 0.0;
+        // rows the refined point violates join the active set -- (no wheel rows) only the most
+        // violated one, and then no row leaves this round: adding every violated row while dropping
+        // every negative multiplier at once cycles on the joint-state envs whose interior point
+        // missed one weakly active pyramid row (a period-3 cycle through 8 rounds, ~1e-4 of the
+        // envs at joint_range 1.0, tests/golden/go2_unrefined_joint_states.npz; tools/kkt_study.py
+        // one_change: every such env settles in <= 4 rounds on its exact optimum)
+        double nviol = 0.0, vl = 0.0, gv[NRL];
 #pragma unroll
         for (int t = 0; t < NRL; ++t) {
-          const bool v = act[t] && Dr[t] == 0.0 && Gv(sVy, t) - h[t] > ytol;
+          gv[t] = Gv(sVy, t) - h[t];
+          vl = fmax(vl, (act[t] && Dr[t] == 0.0 && gv[t] > ytol) ? gv[t] : 0.0);
+        }
+        const double vbest = WHR ? 0.0 : row_max(vl);
+#pragma unroll
+        for (int t = 0; t < NRL; ++t) {
+          const bool v = act[t] && Dr[t] == 0.0 && gv[t] > ytol && (WHR || gv[t] == vbest);
           Dr[t] = v ? dpen : Dr[t];
           nviol += v ? 1.0 : 0.0;
         }
         {
           // ... and rows whose multiplier came out negative leave it (WH: its slack-based active
           // set can include a row the optimum leaves; otherwise a row the interior point's
-          // lambda > s test took with a vanishing multiplier)
-          double mmax = 0.0;
-#pragma unroll
-          for (int t = 0; t < NRL; ++t) mmax = fmax(mmax, Dr[t] != 0.0 ? fabs(mur[t]) : 0.0);
-          const double mtol = 1e-9 * (1.0 + row_max(mmax));
+          // lambda > s test took with a vanishing multiplier) -- (no wheel rows) in a round that
+          // added none, and only the most negative one
+          const bool drops = WHR || vbest == 0.0;   // (uniform over the env's row of lanes)
+          double mmax = 0.0, mlo = 0.0;
 #pragma unroll
           for (int t = 0; t < NRL; ++t) {
-            const bool leave = Dr[t] != 0.0 && mur[t] < -mtol;
+            mmax = fmax(mmax, Dr[t] != 0.0 ? fabs(mur[t]) : 0.0);
+            mlo = fmin(mlo, Dr[t] != 0.0 ? mur[t] : 0.0);
+          }
+          const double mtol = 1e-9 * (1.0 + row_max(mmax));
+          const double mworst = WHR ? 0.0 : row_min(mlo);
+#pragma unroll
+          for (int t = 0; t < NRL; ++t) {
+            const bool leave = drops && Dr[t] != 0.0 && mur[t] < -mtol && (WHR || mur[t] == mworst);
             Dr[t] = leave ? 0.0 : Dr[t];
             // (its multiplier leaves with it: the residual sums G'mu over every row slot, and a
             // stale negative multiplier there would move the next round's fixed point off the

@@ -7,15 +7,37 @@ namespace osc {
 
 // one env per 64-lane wavefront (four envs per wavefront measured no faster: Go2 4,096
 // 35.3 vs 33.7 us)
+// (past one round of interior-point waves the lean variant: osc_setup.hpp setup_env's LEAN; it
+// differs only where phase B runs the 2x2-tile loop, i.e. not for the MFMA models)
 template <class D>
 void launch_setup(const LaunchArgs& a) {
-  hipLaunchKernelGGL(osc_setup_kernel<D>, dim3(static_cast<unsigned>(a.nenv)), dim3(kWave), 0, a.s,
-                     a.model->dparams, a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
+  const dim3 grid(static_cast<unsigned>(a.nenv));
+  if (!D::JG && a.nenv > a.model->small_batch_max)
+    hipLaunchKernelGGL((osc_setup_kernel<D, !D::JG>), grid, dim3(kWave), 0, a.s, a.model->dparams,
+                       a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
+  else
+    hipLaunchKernelGGL((osc_setup_kernel<D, false>), grid, dim3(kWave), 0, a.s, a.model->dparams,
+                       a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
 }
 
 template void launch_setup<Go2>(const LaunchArgs&);
 template void launch_setup<Walter>(const LaunchArgs&);
 template void launch_setup<WalterW>(const LaunchArgs&);
+
+#ifdef OSC_FUSED_TICK
+// the fused joint-state tick: the same assembly with the kinematics in its prologue (A/B builds
+// only: measured slower than the two-kernel tick, osc_kinematics.hip solve_qpos)
+template <class D>
+void launch_setup_qpos(const LaunchArgs& a, const QposArgs& q) {
+  const size_t lds = sizeof(double) * static_cast<size_t>(kin_lds_doubles<D>(q.nq, q.nbody));
+  hipLaunchKernelGGL(osc_setup_qpos_kernel<D>, dim3(static_cast<unsigned>(a.nenv)), dim3(kWave),
+                     lds, a.s, a.model->dparams, a.nenv, q.kin, q.qpos, q.qvel, a.T, a.mask, a.ws,
+                     a.wdir);
+}
+
+template void launch_setup_qpos<Go2>(const LaunchArgs&, const QposArgs&);
+template void launch_setup_qpos<Walter>(const LaunchArgs&, const QposArgs&);
+#endif
 
 }  // namespace osc
 

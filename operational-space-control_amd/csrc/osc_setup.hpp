@@ -5,6 +5,7 @@
 // osc_setup.hip and osc_multi.hip.
 #pragma once
 #include "osc_device.hpp"
+#include "osc_kin_device.hpp"
 
 namespace osc {
 
@@ -95,12 +96,25 @@ __device__ __noinline__ void wave_mgs_lds(double* rows, int nrows, int stride, i
 // The body of one setup wavefront (env = its block index); `sm` is the block's D::SMEM doubles
 // of LDS.  Wrapped by osc_setup_kernel (one model) and osc_setup_pair_kernel (two models, one
 // grid: BASELINE configs[4]).
-template <class D>
+// KIN = true: the fused joint-state tick -- Phase A is the kinematics front end
+// (osc_kin_device.hpp: the same arithmetic as osc_kinematics_kernel) for this env on all 64 lanes,
+// from its qpos / qvel straight into the LDS layout Phase A would have staged M, C, J, b - t into
+// (and, WaLTER, Phase B's J fragments into registers): M, C, J, b never go through HBM.  The
+// kinematics' model tables and per-env state live in the region phases B-D use later (from
+// D::O_HA), so the fused kernel needs kin_lds_doubles<D>() of LDS.
+// LEAN = true (batches past one round of interior-point waves): phase B's 2x2-tile loop unrolled
+// 4 deep instead of fully -- 100 VGPRs instead of 256 (Go2), so three waves share a SIMD; slower
+// where every wave is resident anyway (Go2 4,096: 0.1646 vs 0.1620 ms per solve), faster where the
+// assembly runs many rounds (8,192: 0.2679 vs 0.2701, 65,536: 1.7265 vs 1.7466;
+// profiles/r05/ab_setup_unroll4.jsonl).
+template <class D, bool KIN = false, bool LEAN = false>
 __device__ __forceinline__ void setup_env(
     const DevParams* __restrict__ P, int env, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
-    double* __restrict__ sm, const double* __restrict__ gwd) {
+    double* __restrict__ sm, const double* __restrict__ gwd,
+    const osc_kin::KinDev* __restrict__ Kg = nullptr, const double* __restrict__ gqpos = nullptr,
+    const double* __restrict__ gqvel = nullptr) {
   constexpr int NV = D::NV, NU = D::NU, NC = D::NC, NS = D::NS, NB = D::NB, NY = D::NY,
                 NY1 = D::NY1, NY1P = D::NY1P, S = D::S, NA = D::NA;
   const int lane = threadIdx.x;
@@ -122,74 +136,197 @@ __device__ __forceinline__ void setup_env(
   static_assert(NV % 2 == 0 && NC % 2 == 0, "16-byte staging needs even nv and nc");
   constexpr int JC0 = 3 * (NS - NC);   // first contact translational row of J
   constexpr int JR0 = D::JG ? JC0 : 0; // first row of J staged (JG: the contact rows only)
-  Batch2<D::JROWS * NV / 2, kWave> bJ;
-  Batch2<NV * NV / 2, kWave> bM;
-  Batch2<NV / 2, kWave> bC;
-  Batch2<NC / 2, kWave> bK;
-  bJ.load(gJ + static_cast<size_t>(env) * S * NV + JR0 * NV, lane);
-  bM.load(gM + static_cast<size_t>(env) * NV * NV, lane);
-  bC.load(gC + static_cast<size_t>(env) * NV, lane);
-  bK.load(gmask + static_cast<size_t>(env) * NC, lane);
-  // JG: phase B's MFMA fragments of J (row 4q + (lane >> 4), column lane & 15) loaded now, in the
-  // same memory latency as the staging loads; e and the row weights go to LDS
+  // JG: phase B's MFMA fragments of J (row 4q + (lane >> 4), column lane & 15)
   constexpr int KSJ = D::JG ? (S + 3) / 4 : 0;
   double jf[KSJ > 0 ? KSJ : 1];
-  {
-    const int lc = lane & 15, lg = lane >> 4;
+  Batch2<NC / 2, kWave> bK;
+  bK.load(gmask + static_cast<size_t>(env) * NC, lane);
+  if constexpr (!KIN) {
+    Batch2<D::JROWS * NV / 2, kWave> bJ;
+    Batch2<NV * NV / 2, kWave> bM;
+    Batch2<NV / 2, kWave> bC;
+    bJ.load(gJ + static_cast<size_t>(env) * S * NV + JR0 * NV, lane);
+    bM.load(gM + static_cast<size_t>(env) * NV * NV, lane);
+    bC.load(gC + static_cast<size_t>(env) * NV, lane);
+    // JG: phase B's MFMA fragments of J loaded now, in the same memory latency as the staging
+    // loads; e and the row weights go to LDS
+    {
+      const int lc = lane & 15, lg = lane >> 4;
 #pragma unroll
-    for (int q = 0; q < KSJ; ++q) {
-      const int r = 4 * q + lg;
-      jf[q] = gJ[static_cast<size_t>(env) * S * NV + (r < S ? r : S - 1) * NV + (lc < NV ? lc : 0)];
+      for (int q = 0; q < KSJ; ++q) {
+        const int r = 4 * q + lg;
+        jf[q] = gJ[static_cast<size_t>(env) * S * NV + (r < S ? r : S - 1) * NV + (lc < NV ? lc : 0)];
+      }
+    }
+    constexpr int TEJ = D::JG ? (S + kWave - 1) / kWave : 0;
+    double ebj[TEJ > 0 ? TEJ : 1], etj[TEJ > 0 ? TEJ : 1], wj[TEJ > 0 ? TEJ : 1];
+#pragma unroll
+    for (int q = 0; q < TEJ; ++q) {
+      const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+      const int half = r / (3 * NS), rr = r % (3 * NS);
+      ebj[q] = gb[static_cast<size_t>(env) * S + r];
+      etj[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+      wj[q] = P->w_row[r];
+    }
+    // A column NV: e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168)
+    constexpr int TE = D::JG ? 0 : (S + kWave - 1) / kWave;   // (JG: e enters phase B's fragments)
+    double eb[TE > 0 ? TE : 1], et[TE > 0 ? TE : 1];
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+      const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+      const int half = r / (3 * NS), rr = r % (3 * NS);
+      eb[q] = gb[static_cast<size_t>(env) * S + r];
+      et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
+    }
+    bJ.store(sA, lane, [](int c) { return (c / (NV / 2)) * (NAP / 2) + c % (NV / 2); });   // J rows -> A rows
+#pragma unroll
+    for (int q = 0; q < TEJ; ++q) {
+      const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+      sA[D::O_E + r] = ebj[q] - etj[q];
+      sA[D::O_W + r] = wj[q];
+    }
+    bM.store(sM, lane);
+    bC.store(sC, lane);
+    bK.store(sMask, lane);
+    if constexpr (D::WH) {
+      // the fallback's raw rows (D::W_RM..W_RD): M, C, J's contact rows from the staged registers,
+      // b's contact rows and the wheel directions straight from global
+      double* wr = ws + static_cast<size_t>(env) * D::WS;
+      bM.store(wr + D::W_RM, lane);
+      bC.store(wr + D::W_RC, lane);
+      bJ.store(wr + D::W_RJ, lane);   // (JG: bJ holds exactly the 3 NC contact rows)
+      static_assert(D::JG && D::JROWS == 3 * NC, "wheel rows: the contact rows are the staged ones");
+      for (int q = lane; q < 3 * NC; q += kWave) wr[D::W_RB + q] = gb[static_cast<size_t>(env) * S + JC0 + q];
+      for (int q = lane; q < 6 * NC; q += kWave) wr[D::W_RD + q] = gwd[static_cast<size_t>(env) * NC * 6 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {   // lanes past S rewrite row S-1 with its own value (no branch)
+      const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
+      sA[r * NAP + NV] = eb[q] - et[q];
+      if (NAP > NA) sA[r * NAP + NA] = 0.0;
+    }
+    wave_sync();
+  } else {
+    // the model tables, then this env's state, in the region phases B-D use later (the mask's
+    // LDS slot lies inside it: stored once the kinematics is done)
+    osc_kin::KinDev* sK = reinterpret_cast<osc_kin::KinDev*>(sm + D::O_HA);
+    {
+      static_assert(sizeof(osc_kin::KinDev) % 16 == 0 && D::O_HA % 2 == 0, "16-byte staging");
+      const uint4* src = reinterpret_cast<const uint4*>(Kg);
+      uint4* dst = reinterpret_cast<uint4*>(sK);
+      for (int i = lane; i < static_cast<int>(sizeof(osc_kin::KinDev) / 16); i += kWave)
+        dst[i] = src[i];
+    }
+    wave_sync();
+    const osc_kin::KinDev* K = sK;
+    const int nq = K->nq;
+    const osc_kin::EnvLayout lay(nq, NV, K->nbody, NS);
+    double* E = sm + D::O_HA + sizeof(osc_kin::KinDev) / 8;
+    for (int i = lane; i < nq; i += kWave) E[lay.q + i] = gqpos[static_cast<size_t>(env) * nq + i];
+    for (int i = lane; i < NV; i += kWave) E[lay.q + nq + i] = gqvel[static_cast<size_t>(env) * NV + i];
+    wave_sync();
+    osc_kin::kin_forward(K, E, lay, lane);    // (lane = body; the tree's levels)
+    osc_kin::kin_backward(K, E, lay, lane);
+    for (int d = lane; d < NV; d += kWave) sC[d] = osc_kin::kin_dof(K, E, lay, d);
+    // sites: position, J-dot qvel -> A's column NV = b - t (JG: the e vector), the row weights
+    double* wr = ws + static_cast<size_t>(env) * D::WS;
+    for (int k = lane; k < NS; k += kWave) {
+      double bp[3], br[3];
+      osc_kin::kin_site(K, E, lay, k, bp, br);
+      const double* Tk = gT + static_cast<size_t>(env) * NS * 6 + k * 6;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int rp = 3 * k + i, rr = 3 * NS + 3 * k + i;
+        if constexpr (D::JG) {
+          sA[D::O_E + rp] = bp[i] - Tk[i];
+          sA[D::O_E + rr] = br[i] - Tk[3 + i];
+        } else {
+          sA[rp * NAP + NV] = bp[i] - Tk[i];
+          sA[rr * NAP + NV] = br[i] - Tk[3 + i];
+          if (NAP > NA) {
+            sA[rp * NAP + NA] = 0.0;
+            sA[rr * NAP + NA] = 0.0;
+          }
+        }
+        if constexpr (D::WH) {   // the fallback's raw b rows (contact sites)
+          if (k >= NS - NC) wr[D::W_RB + 3 * (k - (NS - NC)) + i] = bp[i];
+        }
+      }
+    }
+    if constexpr (D::JG) {
+      for (int r = lane; r < S; r += kWave) sA[D::O_W + r] = P->w_row[r];
+    }
+    wave_sync();
+    // M (lane = column j, rows of one parity per half-wave) and J (lane = column c, sites of one
+    // parity per half-wave) from the dofs' S, F
+    {
+      const int j = lane & 31, par = lane >> 5;
+      const bool vj = j < NV;
+      const double* Dj = E + lay.dof + osc_kin::kDofStride * (vj ? j : 0);
+      double Sj[6], Fj[6];
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        Sj[t] = Dj[t];
+        Fj[t] = Dj[6 + t];
+      }
+      for (int i = par; i < NV; i += 2) {
+        const double* Di = E + lay.dof + osc_kin::kDofStride * i;
+        double Si[6], Fi[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          Si[t] = Di[t];
+          Fi[t] = Di[6 + t];
+        }
+        const double m = osc_kin::kin_m_entry(K->dof_relmask[i], K->dof_arm[i], i, j, Si, Fi, Sj, Fj);
+        if (vj) sM[i * NV + j] = m;
+      }
+      // J rows in A (JG: only the contact sites' translational rows, which phase C reads)
+      for (int k = (D::JG ? NS - NC : 0) + par; k < NS; k += 2) {
+        const double* xs = E + lay.site + 3 * k;
+        const double xk[3] = {xs[0], xs[1], xs[2]};
+        double jp[3], jr[3];
+        osc_kin::kin_j_col(vj && ((K->site_dofmask[k] >> j) & 1u), Sj, xk, jp, jr);
+        if (vj) {
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            sA[(3 * k + t - JR0) * NAP + j] = jp[t];
+            if (!D::JG) sA[(3 * NS + 3 * k + t) * NAP + j] = jr[t];
+          }
+        }
+      }
+      if constexpr (D::JG) {
+        // phase B's fragments: J[4q + (lane >> 4)][lane & 15] (rows past S: row S-1; columns past
+        // NV: column 0 -- as the staged loads read them)
+        const int lc = lane & 15, lg = lane >> 4;
+        const int c = lc < NV ? lc : 0;
+        const double* Dc = E + lay.dof + osc_kin::kDofStride * c;
+        double Sc[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) Sc[t] = Dc[t];
+#pragma unroll
+        for (int q = 0; q < KSJ; ++q) {
+          const int r0 = 4 * q + lg, r = r0 < S ? r0 : S - 1;
+          const int half = r / (3 * NS), rr = r % (3 * NS), k = rr / 3, t = rr % 3;
+          const double* xs = E + lay.site + 3 * k;
+          const double xk[3] = {xs[0], xs[1], xs[2]};
+          double jp[3], jr[3];
+          osc_kin::kin_j_col((K->site_dofmask[k] >> c) & 1u, Sc, xk, jp, jr);
+          jf[q] = half ? jr[t] : jp[t];
+        }
+      }
+    }
+    wave_sync();
+    bK.store(sMask, lane);
+    wave_sync();
+    if constexpr (D::WH) {
+      // the fallback's raw rows (D::W_RM..): M, C, J's contact rows from LDS, the directions
+      for (int q = lane; q < NV * NV; q += kWave) wr[D::W_RM + q] = sM[q];
+      for (int q = lane; q < NV; q += kWave) wr[D::W_RC + q] = sC[q];
+      for (int q = lane; q < 3 * NC * NV; q += kWave)
+        wr[D::W_RJ + q] = sA[(q / NV) * NAP + q % NV];   // (JG: A holds exactly the contact rows)
+      for (int q = lane; q < 6 * NC; q += kWave) wr[D::W_RD + q] = gwd[static_cast<size_t>(env) * NC * 6 + q];
     }
   }
-  constexpr int TEJ = D::JG ? (S + kWave - 1) / kWave : 0;
-  double ebj[TEJ > 0 ? TEJ : 1], etj[TEJ > 0 ? TEJ : 1], wj[TEJ > 0 ? TEJ : 1];
-#pragma unroll
-  for (int q = 0; q < TEJ; ++q) {
-    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
-    const int half = r / (3 * NS), rr = r % (3 * NS);
-    ebj[q] = gb[static_cast<size_t>(env) * S + r];
-    etj[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
-    wj[q] = P->w_row[r];
-  }
-  // A column NV: e = b - t,  t = [T[:,0:3] row-wise ; T[:,3:6] row-wise]  (autogen.py:163-168)
-  constexpr int TE = D::JG ? 0 : (S + kWave - 1) / kWave;   // (JG: e enters phase B's fragments)
-  double eb[TE > 0 ? TE : 1], et[TE > 0 ? TE : 1];
-#pragma unroll
-  for (int q = 0; q < TE; ++q) {
-    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
-    const int half = r / (3 * NS), rr = r % (3 * NS);
-    eb[q] = gb[static_cast<size_t>(env) * S + r];
-    et[q] = gT[static_cast<size_t>(env) * NS * 6 + (rr / 3) * 6 + half * 3 + rr % 3];
-  }
-  bJ.store(sA, lane, [](int c) { return (c / (NV / 2)) * (NAP / 2) + c % (NV / 2); });   // J rows -> A rows
-#pragma unroll
-  for (int q = 0; q < TEJ; ++q) {
-    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
-    sA[D::O_E + r] = ebj[q] - etj[q];
-    sA[D::O_W + r] = wj[q];
-  }
-  bM.store(sM, lane);
-  bC.store(sC, lane);
-  bK.store(sMask, lane);
-  if constexpr (D::WH) {
-    // the fallback's raw rows (D::W_RM..W_RD): M, C, J's contact rows from the staged registers,
-    // b's contact rows and the wheel directions straight from global
-    double* wr = ws + static_cast<size_t>(env) * D::WS;
-    bM.store(wr + D::W_RM, lane);
-    bC.store(wr + D::W_RC, lane);
-    bJ.store(wr + D::W_RJ, lane);   // (JG: bJ holds exactly the 3 NC contact rows)
-    static_assert(D::JG && D::JROWS == 3 * NC, "wheel rows: the contact rows are the staged ones");
-    for (int q = lane; q < 3 * NC; q += kWave) wr[D::W_RB + q] = gb[static_cast<size_t>(env) * S + JC0 + q];
-    for (int q = lane; q < 6 * NC; q += kWave) wr[D::W_RD + q] = gwd[static_cast<size_t>(env) * NC * 6 + q];
-  }
-#pragma unroll
-  for (int q = 0; q < TE; ++q) {   // lanes past S rewrite row S-1 with its own value (no branch)
-    const int r = (lane + q * kWave < S) ? lane + q * kWave : S - 1;
-    sA[r * NAP + NV] = eb[q] - et[q];
-    if (NAP > NA) sA[r * NAP + NA] = 0.0;
-  }
-  wave_sync();
 
   STAMP_END(0);
   STAMP_BEGIN();
@@ -272,7 +409,7 @@ __device__ __forceinline__ void setup_env(
     // (fully unrolled: unrolled 4 or 8 deep it needs 100 VGPRs instead of 256 and the CU takes 11
     // setup waves instead of 8, but the kernel is issue-bound and gets slower, 31.6 -> 34.5 us;
     // profiles/r04y/)
-    for (int r = 0; r < S; ++r) {
+    auto ha_row = [&](int r) {
       const double2 x = *reinterpret_cast<const double2*>(sA + r * NAP + i0);
       const double2 y = *reinterpret_cast<const double2*>(sA + r * NAP + j0);
       const double w = P->w_row[r];
@@ -281,6 +418,12 @@ __device__ __forceinline__ void setup_env(
       a01 = fma(wx0, y.y, a01);
       a10 = fma(wx1, y.x, a10);
       a11 = fma(wx1, y.y, a11);
+    };
+    if constexpr (LEAN) {
+#pragma unroll 4
+      for (int r = 0; r < S; ++r) ha_row(r);
+    } else {
+      for (int r = 0; r < S; ++r) ha_row(r);   // (fully unrolled by the compiler)
     }
     put_ha(i0, j0, a00);
     put_ha(i0, j0 + 1, a01);
@@ -725,14 +868,35 @@ __device__ __forceinline__ void setup_env(
 
 // The assembly grid maps block b to env b: an XCD-aware order that put each env's assembly on
 // the XCD of its interior-point block measured no change (Go2 4,096 0.1819 vs 0.1815 ms).
-template <class D>
+template <class D, bool LEAN = false>
 __global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
     const double* __restrict__ gwd) {
   __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
-  setup_env<D>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws, sm, gwd);
+  setup_env<D, false, LEAN>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws,
+                            sm, gwd);
+}
+
+// The fused joint-state tick's assembly (setup_env<D, true>): kinematics from qpos / qvel in the
+// prologue.  LDS: kin_lds_doubles(...) doubles, dynamic (the kinematics' per-env state depends on
+// the tree).
+extern __shared__ __attribute__((aligned(16))) double osc_setup_qpos_sm[];
+template <class D>
+__global__ __launch_bounds__(kWave, 2) void osc_setup_qpos_kernel(
+    const DevParams* __restrict__ P, int nenv, const osc_kin::KinDev* __restrict__ Kg,
+    const double* __restrict__ gqpos, const double* __restrict__ gqvel,
+    const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
+    const double* __restrict__ gwd) {
+  setup_env<D, true>(P, static_cast<int>(blockIdx.x), nenv, nullptr, nullptr, nullptr, nullptr, gT,
+                     gmask, ws, osc_setup_qpos_sm, gwd, Kg, gqpos, gqvel);
+}
+template <class D>
+inline int kin_lds_doubles(int nq, int nbody) {
+  const int kin = D::O_HA + static_cast<int>(sizeof(osc_kin::KinDev) / 8) +
+                  osc_kin::EnvLayout(nq, D::NV, nbody, D::NS).size;
+  return kin > D::SMEM ? kin : D::SMEM;
 }
 
 // Two models' setup in one grid (BASELINE configs[4]: Go2 + WaLTER on one GPU): blocks

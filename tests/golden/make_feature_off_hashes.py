@@ -13,7 +13,9 @@ round: results no longer depend on which envs share a wavefront); the wheel rows
 reach models without them.  Regenerated once in round 4 (profiles/run_r04d.sh) for the
 refinement accepted on a KKT test instead of a per-lane move bound, the interior point's earlier
 stops (Go2 eps_mu 1e-6, WaLTER 1e-8) and the multipliers of rows leaving the refinement's active
-set zeroed.  Regenerate
+set zeroed.  Regenerated once in round 5 (profiles/run_r05h.sh) for the
+refinement's one-change rounds (the most violated row joins, else the most negative multiplier
+leaves: tests/golden/go2_unrefined_joint_states.npz).  Regenerate
 only for an intentional numerical change of the default kernels, and say so in the commit.
 """
 from __future__ import annotations

@@ -23,6 +23,8 @@ Checks (stated tolerances):
     own kinematics within the 1e-5 contract;
   * ten consecutive 4,096-env ticks (cold and warm-started) with every status OK.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -107,6 +109,31 @@ def test_joint_state_batch(gpu, robot, nenv, jr, mask_mode):
         chain.append(torque(model, solve_exact(model, build_qp(model, *ao), Mo, Co, Jo).x))
     nwc, _ = _rel_errors(tau[envs[:16]], np.array(chain))
     assert nwc.max() <= CONTRACT, nwc.max()
+
+
+@pytest.mark.parametrize("seed", [11, 13, 14])
+def test_joint_state_census_every_env_refined(gpu, seed):
+    """Round 5's status census batches (tools/status_diag.py): 65,536 Go2 envs from joint states
+    (joint_range 1.0), where 1 / 4 / 7 envs came back OSC_SOLVE_UNREFINED before the refinement's
+    one-change rounds (their inputs and exact optima: tests/golden/go2_unrefined_joint_states.npz)
+    -- every env OK now, and those envs' torques at the exact optimum."""
+    robot, nenv = "unitree_go2", 65536
+    tree, kb, solver = _setup(robot)
+    qpos, qvel = random_states(tree, nenv, seed, joint_range=1.0)
+    d = generate(robot, nenv, seed, "standing", "ones")
+    k = kb.compute(qpos, qvel, want_sites=False)
+    args = solver.prepare(k.M, k.C, k.J, k.b, d["T"], d["mask"])
+    out = solver.alloc_outputs(nenv)
+    solver.solve_into(out, *args)
+    torch.cuda.synchronize()
+    st = out.status.cpu().numpy()
+    assert (st == 0).all(), (np.bincount(st), np.nonzero(st)[0][:20])
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "go2_unrefined_joint_states.npz"))
+    sel = g["seed"] == seed
+    envs = g["envs"][sel]
+    np.testing.assert_allclose(k.M.cpu().numpy()[envs], g["M"][sel], rtol=0, atol=1e-12)
+    nw, el = _rel_errors(out.tau.cpu().numpy()[envs], g["tau"][sel])
+    assert nw.max() <= NORM_ACH and el.max() <= ELEM_ACH, (nw.max(), el.max())
 
 
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])

@@ -131,10 +131,13 @@ NU_STOP = 12   # torque entries of y in torque coordinates (Go2) for the "ustop"
 TRACE = None   # set to a list to record (it, mu, a_aff, a, alpha, sigma) per iteration
 
 
-def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
+def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=(), init=None):
+    """init: (y, s, lam) -- a warm start (tools/warm_model.py) instead of the cold start."""
     m = len(h)
     small = np.abs(h) < 1e3
-    if "y0_nofz" in variant:                   # least-squares start without the fz <= big rows
+    if init is not None:
+        y, s, lam = (np.array(v, dtype=np.float64) for v in init)
+    elif "y0_nofz" in variant:                   # least-squares start without the fz <= big rows
         keep = ~np.isclose(h, BIG_NUMBER)
         Gs, hs = G[keep], h[keep]
         y = np.linalg.solve(Hr + Gs.T @ Gs, -g + Gs.T @ hs)
@@ -147,7 +150,9 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=()):
         K0 = Hr + G.T @ G
         y = np.linalg.solve(K0, -g + G.T @ h)
     zr = G @ y - h
-    if "mehrotra_init" in variant:
+    if init is not None:
+        pass
+    elif "mehrotra_init" in variant:
         s, lam = -zr.copy(), zr.copy()
         ds_ = max(-1.5 * s.min(), 0.0); dl_ = max(-1.5 * lam.min(), 0.0)
         s += ds_; lam += dl_

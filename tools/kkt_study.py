@@ -146,7 +146,7 @@ def refine_sim(nenv=512, jr=0.5, so=7, envs=None, pens=(1e2, 1e4, 1e6), steps=12
 
 
 def refine_new(Hr, G, h, resid, y, s, lam, pen=1e2, steps_min=2, steps_max=8, rounds=4,
-               restart=True, neg_leave=True):
+               restart=True, neg_leave=True, one_change=False):
     """Candidate kernel refinement: method of multipliers on the active set with the factored
     residual, steps until converged, rows added (violated) / removed (negative multiplier) per
     round; accepted on a KKT test instead of a move bound.  Returns (y, ok, info)."""
@@ -180,6 +180,16 @@ def refine_new(Hr, G, h, resid, y, s, lam, pen=1e2, steps_min=2, steps_max=8, ro
         neg = A & (mu < -mtol) if neg_leave else np.zeros_like(A)
         if conv and not viol.any() and not neg.any():
             return ya, True, info
+        if one_change:   # the most violated row joins, else the most negative multiplier leaves
+            if viol.any():
+                v = np.where(viol, G @ ya - h, -np.inf)
+                viol = np.zeros_like(A)
+                viol[np.argmax(v)] = True
+                neg = np.zeros_like(A)
+            elif neg.any():
+                m = np.where(neg, mu, np.inf)
+                neg = np.zeros_like(A)
+                neg[np.argmin(m)] = True
         A = (A | viol) & ~neg
         mu = np.where(A, mu, 0.0)
     return ya, False, info
