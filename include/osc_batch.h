@@ -77,7 +77,9 @@ typedef enum {
 typedef enum {
   OSC_SOLVE_OK = 0,               /* converged: complementarity <= eps_mu                     */
   OSC_SOLVE_MAX_ITER = 1,         /* iteration cap reached; best iterate returned             */
-  OSC_SOLVE_NUMERICAL = 2,        /* non-finite values encountered (e.g. NaN inputs)         */
+  OSC_SOLVE_NUMERICAL = 2,        /* non-finite values encountered (e.g. NaN inputs), or an M
+                                     that is not positive definite (a pivot <= 0 in the
+                                     elimination of dv; every mass matrix is SPD)              */
   OSC_SOLVE_UNREFINED = 3         /* converged (complementarity <= eps_mu) but the full-space
                                      refinement found no KKT point within its rounds (or was
                                      forced off by osc_model_tuning.refine_max_move): the
@@ -231,8 +233,9 @@ int osc_batch_solve_assembled(const osc_model* model, int32_t nenv, const double
  * Results agree with the cold solve to the solve's tolerance; the iteration count drops when
  * consecutive ticks are close.  A warm env that stalls is re-centred in place,
  * and any env the warm pass leaves not OK (OSC_SOLVE_MAX_ITER / _NUMERICAL / _UNREFINED) is
- * re-solved cold, to mu <= 1e-12, by a second launch that only the wavefronts holding such an env
- * execute. */
+ * re-solved cold, to mu <= 1e-12, by the wavefront holding it right after its warm pass (the
+ * same launch; past one wave per SIMD without wheel rows: a second launch that only the
+ * wavefronts holding such an env execute). */
 int osc_warm_state_bytes(const osc_model* model, int32_t nenv, size_t* bytes);
 int osc_batch_solve_warm(const osc_model* model, int32_t nenv,
                          const double* M, const double* C, const double* J, const double* b,

@@ -1642,8 +1642,19 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : OSC_LARGE_WAVES) void osc_ipm_ke
                 "IPM LDS");
   static_assert(ipm_lds_doubles<D, SMALL, RF>() * 8 <= 64 * 1024, "IPM LDS per workgroup");
   __shared__ __attribute__((aligned(16))) double sm[ipm_lds_doubles<D, SMALL, RF>()];
+  // flags bit 2 (warm-started, refinement fused): the cold fix-up pass runs in the same launch,
+  // each wavefront right after its own warm pass (its statuses are its own global stores: the
+  // fence makes them visible to its lanes) -- the separate fix-up launch, 1,024 wavefronts that
+  // mostly exit at once, cost 4.2 us of a 139 us Go2 4,096 warm tick
   ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
-                                    gstatus, giters, gwarm, flags, sm);
+                                gstatus, giters, gwarm, flags & 3, sm);
+  if constexpr (WARM) {
+    if (flags & 4) {   // (a second inlined body: a loop over both passes spilled 180 B per lane)
+      __threadfence();
+      ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
+                                    gstatus, giters, gwarm, (flags & 2) | 1, sm);
+    }
+  }
 }
 
 // The cold fused solve split in two passes for lockstep compaction (ParkArgs): CP = kCpPark
@@ -1706,17 +1717,15 @@ void launch_ipm(const LaunchArgs& a) {
   const int flags = a.y != nullptr ? 2 : 0;   // hand the multipliers to the dual kernel
   if constexpr (D::WH) {
     // wheel rows: the one-wave solve with the refinement fused; warm-started: the warm pass, then
-    // the cold fix-up pass over the wavefronts holding an env the warm start left unconverged (the
-    // per-env status: the caller's array, else scratch -- launch_t).  The fused entries then run
+    // (same launch) the cold fix-up pass in the wavefronts holding an env the warm start left
+    // unconverged (the per-env status: the caller's array, else scratch -- launch_t).  The fused entries then run
     // the active-set fallback over the envs the interior point left unconverged (launch_gi).
     if (warm == nullptr) {
       hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
                          model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
     } else {
-      for (int pass = 0; pass < 2; ++pass)
-        hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, warm,
-                           flags | pass);
+      hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                         model->dparams, nenv, mask, ws, tau, x, status, iters, warm, flags | 4);
     }
   } else {
     // A warm-started solve is followed by a cold fix-up pass over the wavefronts that hold an
@@ -1769,12 +1778,11 @@ void launch_ipm(const LaunchArgs& a) {
         hipLaunchKernelGGL((osc_ipm_kernel<D, false, false>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
     } else if (fused_warm) {
-      // warm-started: the refinement runs in the same wavefront too, in pass 0 for the envs the
-      // warm start converged and in the cold fix-up pass for the ones it redoes
-      for (int pass = 0; pass < 2; ++pass) {
-        hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, warm, pass);
-      }
+      // warm-started: the refinement runs in the same wavefront too, in the warm pass for the
+      // envs the warm start converged and in the cold fix-up pass (same launch) for the ones it
+      // redoes
+      hipLaunchKernelGGL((osc_ipm_kernel<D, true, true, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                         model->dparams, nenv, mask, ws, tau, x, status, iters, warm, 4);
     } else {
       // warm past one wave per SIMD (or without the refinement): the warm pass, the separate
       // refinement pass, then the cold fix-up pass over every env not OK by then -- MAX_ITER,

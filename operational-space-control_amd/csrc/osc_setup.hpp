@@ -468,7 +468,9 @@ __device__ __forceinline__ void setup_env(
       for (int j = 0; j <= i; ++j) L[i][j] = sM[i * NV + j];
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      dinv[k] = recip1(L[k][k]);
+      // a pivot <= 0: M is not positive definite (no mass matrix is) -- NaN poisons X, so the
+      // env comes back OSC_SOLVE_NUMERICAL instead of an interior point on a meaningless reduction
+      dinv[k] = L[k][k] > 0.0 ? recip1(L[k][k]) : __builtin_nan("");
 #pragma unroll
       for (int i = k + 1; i < NB; ++i) {          // trailing update with the unscaled column
         const double lik = L[i][k] * dinv[k];
@@ -535,7 +537,8 @@ __device__ __forceinline__ void setup_env(
     double dj = 1.0;
     static_for<0, NU>([&](auto K) {
       constexpr int k = decltype(K)::value;
-      const double rk = recip1(bcast_guarded<k>(col[k]));       // 1 / S_k[k][k]
+      const double pk = bcast_guarded<k>(col[k]);
+      const double rk = pk > 0.0 ? recip1(pk) : __builtin_nan("");   // 1 / S_k[k][k] (M SPD)
       if (lj == k) dj = rk;
       const double m = (lj > k) ? -col[k] * rk : 0.0;          // -S_k[k][j] / d_k, lanes j > k
       static_for<k + 1, NU>([&](auto I) {

@@ -202,3 +202,13 @@ def test_edge_cases(gpu):
     st = res.status.cpu().numpy()
     assert st[2] == 2 and (st[[0, 1, 3]] == 0).all()
     assert torch.equal(res.tau[[0, 1, 3]], res4.tau[[0, 1, 3]])
+    # so does an M that is not positive definite (no mass matrix is; the reduction eliminates
+    # dv through M's LDL^T pivots): env 1's shifted to a smallest eigenvalue of -0.05
+    d3 = {k: v.copy() for k, v in d.items()}
+    lo = np.linalg.eigvalsh(d3["M"][1])[0]
+    d3["M"][1] -= (lo + 0.05) * np.eye(d3["M"].shape[1])
+    res = s.solve(**d3)
+    torch.cuda.synchronize()
+    st = res.status.cpu().numpy()
+    assert st[1] == 2 and (st[[0, 2, 3]] == 0).all(), st
+    assert torch.equal(res.tau[[0, 2, 3]], res4.tau[[0, 2, 3]])

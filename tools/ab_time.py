@@ -9,6 +9,8 @@ so older builds load too).  Diagnostic only.
                      solves per library after 5 warmup solves; the JSON lines give each round,
                      the summary line the median per library and configuration
     AB_CHECK=1       also compare each library's torques with the first one's (bitwise flag)
+    AB_WARM=1        warm-started ticks instead (osc_batch_solve_warm, the warm state carried,
+                     inputs alternating between the batch and a 1 % perturbed copy)
 """
 import ctypes
 import json
@@ -44,6 +46,8 @@ class Lib:
         self.path = path
         self.L = ctypes.CDLL(path)
         self.L.osc_batch_solve.argtypes = [vp, ctypes.c_int32] + [vp] * 10 + [vp, ctypes.c_size_t, vp]
+        self.L.osc_batch_solve_warm.argtypes = [vp, ctypes.c_int32] + [vp] * 10 + \
+            [vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp]
         self.models = {}
 
     def model(self, robot):
@@ -61,11 +65,24 @@ def main():
     libs = [Lib(p) for p in sys.argv[1:]]
     rounds = int(os.environ.get("AB_ROUNDS", "3"))
     check = os.environ.get("AB_CHECK") == "1"
+    warm_mode = os.environ.get("AB_WARM") == "1"
     times = {}
     for robot, nenv in configs():
         g = generate(robot, nenv, SEED_BASE + 2)
         t = [torch.from_numpy(g[k]).cuda().contiguous() for k in ("M", "C", "J", "b", "T", "mask")]
         p = [vp(x.data_ptr()) for x in t]
+        gen = torch.Generator(device="cuda").manual_seed(5)
+        t2 = [x if i == 5 else (x * (1.0 + 0.01 * torch.randn(x.shape, generator=gen, device="cuda",
+                                                               dtype=x.dtype))).contiguous()
+              for i, x in enumerate(t)]
+        # M by a congruence A M A' (SPD kept; an elementwise 1 % perturbation made ~1 % of the
+        # WaLTER M indefinite or near-singular: unphysical QPs the reduction flags)
+        nv = t[0].shape[1]
+        A = torch.eye(nv, dtype=torch.float64, device="cuda") + 0.01 / nv ** 0.5 * torch.randn(
+            t[0].shape, generator=gen, device="cuda", dtype=torch.float64)
+        t2[0] = A @ t[0] @ A.transpose(1, 2)
+        t2[0] = (0.5 * (t2[0] + t2[0].transpose(1, 2))).contiguous()
+        p2 = [vp(x.data_ptr()) for x in t2]
         nu = {"unitree_go2": 12, "walter_sr": 8}[robot]
         taus = []
         for lib in libs:
@@ -73,15 +90,29 @@ def main():
             lib.L.osc_workspace_bytes(lib.model(robot), nenv, ctypes.byref(nb))
             lib.ws = torch.empty((nb.value // 8 + 2,), dtype=torch.float64, device="cuda")
             lib.tau = torch.empty((nenv, nu), dtype=torch.float64, device="cuda")
+            if warm_mode:
+                wb = ctypes.c_size_t()
+                lib.L.osc_warm_state_bytes(lib.model(robot), nenv, ctypes.byref(wb))
+                lib.warm = torch.zeros((wb.value // 8 + 2,), dtype=torch.float64, device="cuda")
+                lib.tick = 0
         for r in range(rounds):
             for lib in libs:
                 h = lib.model(robot)
 
                 def call():
-                    rc = lib.L.osc_batch_solve(h, nenv, *p, vp(lib.tau.data_ptr()), None, None,
-                                               None, vp(lib.ws.data_ptr()),
-                                               ctypes.c_size_t(lib.ws.numel() * 8),
-                                               vp(torch.cuda.current_stream().cuda_stream))
+                    if warm_mode:
+                        lib.tick += 1
+                        rc = lib.L.osc_batch_solve_warm(
+                            h, nenv, *(p if lib.tick % 2 else p2), vp(lib.tau.data_ptr()), None,
+                            None, None, vp(lib.warm.data_ptr()),
+                            ctypes.c_size_t(lib.warm.numel() * 8), vp(lib.ws.data_ptr()),
+                            ctypes.c_size_t(lib.ws.numel() * 8),
+                            vp(torch.cuda.current_stream().cuda_stream))
+                    else:
+                        rc = lib.L.osc_batch_solve(h, nenv, *p, vp(lib.tau.data_ptr()), None, None,
+                                                   None, vp(lib.ws.data_ptr()),
+                                                   ctypes.c_size_t(lib.ws.numel() * 8),
+                                                   vp(torch.cuda.current_stream().cuda_stream))
                     assert rc == 0
                 for _ in range(5):
                     call()
