@@ -550,31 +550,49 @@ __device__ __forceinline__ void ipm_block(
   // coordinate i at a time -- column j gains coef_i(j) T[i][:], coef_i(j) = (G'DG)[i][:] T[:][j]
   // (torque rows: diagonal; a contact's rows: its 3 x 3 block) -- then pin Q's coordinates.
   // Returns the assembled diagonal entries (the pivot threshold's reference).
-  auto assemble_rot = [&](double& dg0r, double& dg1r) {
+  auto assemble_rot = [&](double& dg0r, double& dg1r) __attribute__((always_inline)) {
     if constexpr (WHR) {
+      // K^ columns j0, jj1 += T' (B T)[:, j] with B = G'DG (diagonal on u, a 3 x 3 block per
+      // contact), one row i of T at a time: a = (B T)[i, j] from the lane's own entries of T, then
+      // c[m] += a T[i][m] with T[i][m] broadcast from the lane that owns column m
+      // (v_fmac_f64_dpp row_newbcast) -- each lane reads its own two entries of row i instead of
+      // the whole row from LDS (the per-iteration product of the wheel rows: NY^3 per env)
+      auto rank1 = [&](double a0, double a1, double t0, double t1) __attribute__((always_inline)) {
+        static_for<0, kRow>([&](auto K) __attribute__((always_inline)) {
+          constexpr int k = decltype(K)::value;
+          if constexpr (k < NY) {
+            fmac_bcast<k, k == 0>(c0[k], t0, a0);
+            fmac_bcast<k>(c1[k], t0, a1);
+          }
+          if constexpr (k + kRow < NY) {
+            fmac_bcast<k, k == 0>(c0[k + kRow], t1, a0);
+            fmac_bcast<k>(c1[k + kRow], t1, a1);
+          }
+        });
+      };
 #pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        double a0, a1;
-        if (i < NU) {
-          const double d = sDr[2 * i] + sDr[2 * i + 1];
-          a0 = d * sWT[i * WL::TST + j0];
-          a1 = d * sWT[i * WL::TST + jj1];
-        } else {
-          const int k = (i - NU) / 3, ci = (i - NU) % 3, zb = NU + 3 * k;
+      for (int i = 0; i < NU; ++i) {
+        const double d = sDr[2 * i] + sDr[2 * i + 1];
+        const double t0 = sWT[i * WL::TST + j0], t1 = sWT[i * WL::TST + jj1];
+        rank1(d * t0, d * t1, t0, t1);
+      }
+      static_for<0, NC>([&](auto Kc) __attribute__((always_inline)) {
+        constexpr int k = decltype(Kc)::value, zb = NU + 3 * k;
+        double t0r[3], t1r[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          t0r[r] = sWT[(zb + r) * WL::TST + j0];
+          t1r[r] = sWT[(zb + r) * WL::TST + jj1];
+        }
+        static_for<0, 3>([&](auto Ci) __attribute__((always_inline)) {
+          constexpr int ci = decltype(Ci)::value;
           double b0, b1, b2;   // row ci of contact k's block (symmetric: its column ci)
           contact_col(k, ci, b0, b1, b2);
-          a0 = b0 * sWT[zb * WL::TST + j0] + b1 * sWT[(zb + 1) * WL::TST + j0] +
-               b2 * sWT[(zb + 2) * WL::TST + j0];
-          a1 = b0 * sWT[zb * WL::TST + jj1] + b1 * sWT[(zb + 1) * WL::TST + jj1] +
-               b2 * sWT[(zb + 2) * WL::TST + jj1];
-        }
-#pragma unroll
-        for (int m = 0; m < NY; ++m) {
-          const double t = sWT[i * WL::TST + m];
-          c0[m] = fma(a0, t, c0[m]);
-          c1[m] = fma(a1, t, c1[m]);
-        }
-      }
+          const double a0 = b0 * t0r[0] + b1 * t0r[1] + b2 * t0r[2];
+          const double a1 = b0 * t1r[0] + b1 * t1r[1] + b2 * t1r[2];
+          rank1(a0, a1, t0r[ci], t1r[ci]);
+        });
+      });
       double d0 = 0.0, d1 = 0.0;
 #pragma unroll
       for (int m = 0; m < NY; ++m) {
