@@ -107,6 +107,13 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
 
     kin_ms = timed(lambda: kb.compute_into(kout, qpos, qvel))
     tick_ms = timed(lambda: kb.solve_into(solver, out, qpos, qvel, T, mask, ws))
+    # the same QPs solved from their M, C, J, b (osc_batch_solve): the tick minus this is what the
+    # kinematics front end adds -- joint-state QPs take more interior-point iterations than the
+    # synthetic headline batch, so the headline's ms_per_step is not the comparison
+    kq = kb.compute(qpos, qvel, want_sites=False)
+    qargs = solver.prepare(kq.M, kq.C, kq.J, kq.b, T, mask)
+    out_q = solver.alloc_outputs(nenv)
+    solve_ms = timed(lambda: solver.solve_into(out_q, *qargs))
     # a control loop: 10 consecutive joint states (joint angles +-0.01 rad, velocities +-1 % per
     # step, base quaternion re-normalised), replayed ping-pong, warm state carried tick to tick
     g = torch.Generator(device=qpos.device).manual_seed(seed + 11)
@@ -138,6 +145,8 @@ def front_end(robot: str, solver, nenv: int, steps: int, warmup: int, seed: int,
                          "frac": gbs / HBM_PEAK_GBS, "bytes_per_env": kin_bytes},
             "tick_from_joint_states_ms": tick_ms,
             "tick_from_joint_states_solves_per_s": nenv / (tick_ms * 1e-3),
+            "solve_same_qps_ms": solve_ms,
+            "kinematics_added_ms": tick_ms - solve_ms,
             "tick_from_joint_states_warm_ms": warm_ms,
             "tick_from_joint_states_warm_solves_per_s": nenv / (warm_ms * 1e-3),
             "tick_from_joint_states_warm_mean_ipm_iters": float(out.iters.double().mean().item())}
