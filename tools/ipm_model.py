@@ -238,6 +238,19 @@ def ipm(Hr, g, G, h, eps_mu=1e-12, max_iter=40, variant=(), init=None):
         if mu <= eps_mu:
             FINAL.update(s=s.copy(), lam=lam.copy())
             return y, it, True
+        asstop = [v for v in variant if v.startswith("asstop")]
+        if asstop:
+            # active-set stop ("asstop<mu>,<k>"): mu <= <mu> and the rows with lambda > s the same
+            # for <k> consecutive iterations -- the refinement takes it from there
+            mth, kk = asstop[0][6:].split(",")
+            act = tuple(np.nonzero(lam > s)[0])
+            hist = FINAL.setdefault("_acts", [])
+            if it == 0:
+                hist.clear()
+            hist.append(act)
+            if mu <= float(mth) and len(hist) > int(kk) and all(a == act for a in hist[-int(kk) - 1:]):
+                FINAL.update(s=s.copy(), lam=lam.copy())
+                return y, it, True
         ustop = [v for v in variant if v.startswith("ustop")]
         if ustop and last_du is not None:
             # torque-coordinate stop: the last step moved the torques y[:NU] by less than
