@@ -71,18 +71,19 @@ def test_warm_state_api_errors(gpu):
         solver.solve_warm_into(out, short, *args)
 
 
-def test_warm_two_wave_fixup_rescues_unrefined(gpu):
-    """past one wave per SIMD the warm solve refines in a separate pass, and an env whose
-    refinement finds no KKT point (OSC_SOLVE_UNREFINED) goes to the cold fix-up pass like a
-    MAX_ITER env (include/osc_batch.h: the warm entry re-solves every env its warm pass leaves
-    not OK).  Forced here: refine_max_move = 0 rejects every refinement, so every env of the
-    8,192-env batch (two rounds of wavefronts: the two-wave kernel) is re-solved cold to
+@pytest.mark.parametrize("nenv", [4096, 8192])
+def test_warm_fixup_rescues_unrefined(gpu, nenv):
+    """an env whose refinement finds no KKT point (OSC_SOLVE_UNREFINED) goes to the cold
+    fix-up pass like a MAX_ITER env (include/osc_batch.h: the warm entry re-solves every env its
+    warm pass leaves not OK) -- at 8,192 (two rounds of wavefronts: the two-wave kernel, which
+    refines in a separate pass, then the fix-up launch) and at 4,096 (the one-wave kernel, whose
+    wavefronts run the fix-up in the same launch right after their warm pass, round 5).  Forced
+    here: refine_max_move = 0 rejects every refinement, so every env is re-solved cold to
     mu <= 1e-12 (iters reported as max_iter + the fix-up's count).  Its refinement is rejected
     again, so it stays UNREFINED -- but the returned iterate is the 1e-12 one, within the 1e-5
     contract of the default solve, not the warm early stop's (up to ~3e-2, test_gpu_wheels::
     test_rejected_refinement_is_reported)."""
     from osc_amd.solver import OSCBatchSolver
-    nenv = 8192
     s = OSCBatchSolver("unitree_go2", tuning={"refine_max_move": 0.0})
     ref = OSCBatchSolver("unitree_go2")
     d = generate("unitree_go2", nenv, SEED_BASE + 23, "tumbling", "bernoulli")
@@ -94,7 +95,7 @@ def test_warm_two_wave_fixup_rescues_unrefined(gpu):
     st, it = out.status.cpu().numpy(), out.iters.cpu().numpy()
     # (UNREFINED everywhere, except an env whose 1e-12 iterate is already the optimum -- its
     # refinement does not move y, which even refine_max_move = 0 accepts: 4 of 8,192 measured)
-    assert np.isin(st, [0, 3]).all() and (st == 3).sum() >= nenv - 64, np.bincount(st)
+    assert np.isin(st, [0, 3]).all() and (st == 3).sum() >= nenv - nenv // 128, np.bincount(st)
     assert (it > s.desc.max_iter).all(), it.min()
     assert (good.status.cpu().numpy() == 0).all()
     tau, gt = out.tau.cpu().numpy(), good.tau.cpu().numpy()
