@@ -85,6 +85,27 @@ void tuning_from_env(osc_model_tuning& t) {
 #endif
 }  // namespace
 
+#ifdef OSC_STAMPS
+// Diagnostic builds only: the phase-cycle buffers every kernel unit's STAMP_STORE writes through
+// DevParams (allocated with the first model), and their readers (tools/stamps.py,
+// tools/setup_stamps.py): [nblocks][kStampSlots] of the last launch.
+namespace {
+unsigned long long* g_stamp_buf[2] = {nullptr, nullptr};
+int stamps_read(int which, unsigned long long* host, int nblocks) {
+  if (!g_stamp_buf[which]) return OSC_ERR_INVALID_ARGUMENT;
+  if (nblocks > kStampBlocks) nblocks = kStampBlocks;
+  return hipMemcpy(host, g_stamp_buf[which], sizeof(unsigned long long) * kStampSlots * nblocks,
+                   hipMemcpyDeviceToHost) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
+}
+}  // namespace
+extern "C" int osc_debug_stamps(unsigned long long* host, int nblocks) {
+  return stamps_read(0, host, nblocks);
+}
+extern "C" int osc_debug_setup_stamps(unsigned long long* host, int nblocks) {
+  return stamps_read(1, host, nblocks);
+}
+#endif
+
 extern "C" int osc_model_tuning_defaults(const osc_model_desc* desc, osc_model_tuning* tuning) {
   if (!desc || !tuning) return OSC_ERR_INVALID_ARGUMENT;
   tuning_defaults(*desc, *tuning);
@@ -175,6 +196,13 @@ extern "C" int osc_model_create_tuned(const osc_model_desc* desc, const osc_mode
     hp.wheel_radius[i] = d.wheel_radius[i];
   }
   hp.wheel_tol = t.wheel_tol;
+#ifdef OSC_STAMPS
+  for (auto*& b : g_stamp_buf)
+    if (!b && hipMalloc(&b, sizeof(unsigned long long) * kStampSlots * kStampBlocks) != hipSuccess)
+      return OSC_ERR_DEVICE;
+  hp.stamps = g_stamp_buf[0];
+  hp.setup_stamps = g_stamp_buf[1];
+#endif
 
   osc_model* m = new (std::nothrow) osc_model;
   if (!m) return OSC_ERR_DEVICE;

@@ -54,6 +54,10 @@ struct DevParams {
   double wheel_radius[OSC_MAX_SITES];
   double wheel_tol;                  // interior point: |row residual| <= wheel_tol to stop
   double refine_max_move;            // a refinement moving y by more (relative) is rejected
+#ifdef OSC_STAMPS
+  unsigned long long* stamps;        // diagnostic builds: [kStampBlocks][kStampSlots], IPM phases
+  unsigned long long* setup_stamps;  // ... and the assembly's (one buffer for every kernel unit)
+#endif
 };
 
 // Full-space refinement: at most kRefineRounds active-set rounds of at most kRefineMaxSteps
@@ -333,12 +337,11 @@ __device__ __forceinline__ double row_max(double v) {
 }
 
 // ---- diagnostic stamps (OSC_STAMPS builds only; the product build compiles them out) ----
-// Per wave, cycles (s_memtime) accumulated per IPM phase; read back by osc_debug_stamps.
+// Per wave, cycles (s_memtime) accumulated per IPM phase into DevParams::stamps (one buffer for
+// every kernel unit: static __device__ arrays were per unit); read back by osc_debug_stamps.
 #ifdef OSC_STAMPS
 constexpr int kStampSlots = 12;
 constexpr int kStampBlocks = 1 << 15;
-static __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
-static __device__ unsigned long long g_setup_stamps[kStampBlocks * kStampSlots];
 #define STAMP_DECL unsigned long long st_acc[kStampSlots] = {}; unsigned long long st_t0 = 0;
 #define STAMP_BEGIN()                                                        \
   do {                                                                       \
@@ -358,13 +361,13 @@ static __device__ unsigned long long g_setup_stamps[kStampBlocks * kStampSlots];
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                       \
       for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
-        g_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];                \
+        P->stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];               \
   } while (0)
 #define STAMP_STORE_SETUP()                                                  \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                       \
       for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
-        g_setup_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];          \
+        P->setup_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];         \
   } while (0)
 #else
 #define STAMP_DECL

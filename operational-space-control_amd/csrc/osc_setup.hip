@@ -40,13 +40,3 @@ template void launch_setup_qpos<Walter>(const LaunchArgs&, const QposArgs&);
 #endif
 
 }  // namespace osc
-
-#ifdef OSC_STAMPS
-// Diagnostic build only: per-block setup phase cycles [nblocks][kStampSlots], slots 0-5 used.
-extern "C" int osc_debug_setup_stamps(unsigned long long* host, int nblocks) {
-  using namespace osc;
-  if (nblocks > kStampBlocks) nblocks = kStampBlocks;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_stamps), sizeof(unsigned long long) *
-                             kStampSlots * nblocks) == hipSuccess ? OSC_OK : OSC_ERR_DEVICE;
-}
-#endif
