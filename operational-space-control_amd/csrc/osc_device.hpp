@@ -163,7 +163,8 @@ struct Dims {
   // WH: Gram-Schmidt of [Q; I_NY] (NW + NY rows of NY) -> the basis T of the y space whose first
   // columns are Q's rows (compacted in place: row k = column k of T)
   static constexpr int O_WT = O_WA + NW * WAST;
-  static constexpr int SMEM = O_WT + (WH ? (NW + NY) * NY : 0);
+  static constexpr int WTST = NY + 1;   // the basis rows' LDS stride (odd: no bank conflicts)
+  static constexpr int SMEM = O_WT + (WH ? (NW + NY) * WTST : 0);
   static_assert(NW <= kRow, "IPM: one wheel row per lane of the env's row");
   static_assert(NV % 2 == 0, "setup: J rows are staged in 16-byte chunks");
   static_assert(SMEM * 8 <= 64 * 1024, "setup LDS budget per env");

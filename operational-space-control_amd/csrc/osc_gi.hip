@@ -2,6 +2,7 @@
 // Idnani's dual method on the full QP of an env the interior point left unconverged (DESIGN.md
 // §3.1; the opt-in rows of walter_sr_wheels/autogen/autogen.py:128-240).
 #include "osc_internal.hpp"
+#include "osc_wave_sum.hpp"
 
 namespace osc {
 
@@ -53,25 +54,11 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   const double* wd = wenv + D::W_RD;
   const double hu = 2.0 * (P->w_torque + P->w_reg), hz = 2.0 * P->w_reg;
 
-  auto wsum = [](double v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
-  };
-  auto wmax = [](double v) {
-    for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
-    return v;
-  };
-  // (value, index) minimum, the lowest index among ties
-  auto wargmin = [](double& v, int& idx) {
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(v, o, kWave);
-      const int oi = __shfl_xor(idx, o, kWave);
-      if (ov < v || (ov == v && oi < idx)) {
-        v = ov;
-        idx = oi;
-      }
-    }
-  };
+  // the 64-lane butterflies (sum, max, (value, index) minimum with the lowest index among ties),
+  // their partners by lane-crossing VALU ops (osc_wave_sum.hpp; the shuffle form's order and bits)
+  auto wsum = [](double v) { return wave_sum_fast(v); };
+  auto wmax = [](double v) { return wave_max_fast(v); };
+  auto wargmin = [](double& v, int& idx) { wave_argmin_fast(v, idx); };
   // one-sided row p (c'x >= b): its coefficient on variable i, right-hand side, max |c|, and
   // whether it exists (finite bound; the fz box only on contacts in touch)
   auto in_coef = [&](int p, int i) -> double {
@@ -390,10 +377,19 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     GI_T0();
     // working one-sided rows as a bit set over p
     unsigned long long in_set = (lane < q && act >= kIneq) ? (1ull << (act - kIneq)) : 0ull;
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const unsigned lo = __shfl_xor(static_cast<unsigned>(in_set), o, kWave);
-      const unsigned hi = __shfl_xor(static_cast<unsigned>(in_set >> 32), o, kWave);
-      in_set |= (static_cast<unsigned long long>(hi) << 32) | lo;
+    {
+      auto orx = [&](auto O) {
+        constexpr int o = decltype(O)::value;
+        const unsigned lo = xor_partner_u32<o>(static_cast<unsigned>(in_set), lane);
+        const unsigned hi = xor_partner_u32<o>(static_cast<unsigned>(in_set >> 32), lane);
+        in_set |= (static_cast<unsigned long long>(hi) << 32) | lo;
+      };
+      orx(std::integral_constant<int, 32>{});
+      orx(std::integral_constant<int, 16>{});
+      orx(std::integral_constant<int, 8>{});
+      orx(std::integral_constant<int, 4>{});
+      orx(std::integral_constant<int, 2>{});
+      orx(std::integral_constant<int, 1>{});
     }
     const double xs = wmax(lane < NX ? fabs(xi) : 0.0);
     double viol = INFINITY;

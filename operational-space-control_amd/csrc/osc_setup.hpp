@@ -6,6 +6,7 @@
 #pragma once
 #include "osc_device.hpp"
 #include "osc_kin_device.hpp"
+#include "osc_wave_sum.hpp"
 
 namespace osc {
 
@@ -14,12 +15,9 @@ namespace osc {
 // FP64 matrix cores (v_mfma_f64_16x16x4f64).
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// Sum over the 64 lanes, the same value on every lane (lane 0's butterfly result broadcast).
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return __shfl(v, 0, kWave);
-}
+// Sum over the 64 lanes, the same value on every lane (the shuffle butterfly's order, its
+// partners by lane-crossing VALU ops: osc_wave_sum.hpp).
+__device__ __forceinline__ double wave_sum(double v) { return wave_sum_fast(v); }
 
 // Modified Gram-Schmidt over the NR rows of an LDS row set (row stride `stride`, `ncol` columns,
 // one lane per column): the first NDOT columns are made orthonormal, the other columns follow the
@@ -63,31 +61,38 @@ __device__ __forceinline__ void wave_mgs(double* rows, int stride, int ncol, int
 // were most of the wheel model's setup: 975 -> 564 us for 2,048 envs), then lane c subtracts them
 // from column c; the second pass restores orthogonality to working precision.  (For the 16-row
 // sets the register-resident wave_mgs above stays: this LDS form measured 2.3x slower there,
-// profiles/r04za/.)  `scf`: nrows doubles of LDS scratch.
-__device__ __noinline__ void wave_mgs_lds(double* rows, int nrows, int stride, int ncol, int ndot,
-                                          int lane, double drop, double* scf) {
-  const bool cv = lane < ncol, dv = lane < ndot;
-  for (int w = 0; w < nrows; ++w) {
-    double aw = cv ? rows[w * stride + lane] : 0.0;
+// profiles/r04za/.)  `scf`: nrows doubles of LDS scratch.  The shape is compile-time so the dot
+// products' and the subtraction's LDS reads are issued ahead of their FMA chains (round 5: the
+// runtime-bounded loops waited on every read, ~3.9k clocks per row pass, 58 % of the wheel
+// model's assembly; the FMA order -- and so every result -- is unchanged).
+template <int NROWS, int STRIDE, int NCOL, int NDOT>
+__device__ __noinline__ void wave_mgs_lds(double* rows, int lane, double drop, double* scf) {
+  const bool cv = lane < NCOL, dv = lane < NDOT;
+  for (int w = 0; w < NROWS; ++w) {
+    double aw = cv ? rows[w * STRIDE + lane] : 0.0;
     const double n0 = sqrt(wave_sum(dv ? aw * aw : 0.0));
     for (int pass = 0; pass < 2 && w > 0; ++pass) {
       double cf = 0.0;
       if (lane < w) {
-        for (int c = 0; c < ndot; ++c) cf = fma(rows[lane * stride + c], rows[w * stride + c], cf);
+        const double* rl = rows + lane * STRIDE;
+        const double* rw = rows + w * STRIDE;
+#pragma unroll
+        for (int c = 0; c < NDOT; ++c) cf = fma(rl[c], rw[c], cf);
       }
       if (lane < w) scf[lane] = cf;
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       if (cv) {
-        for (int v = 0; v < w; ++v) aw = fma(-scf[v], rows[v * stride + lane], aw);
-        rows[w * stride + lane] = aw;
+#pragma unroll 8
+        for (int v = 0; v < w; ++v) aw = fma(-scf[v], rows[v * STRIDE + lane], aw);
+        rows[w * STRIDE + lane] = aw;
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
     }
     const double nn = sqrt(wave_sum(dv ? aw * aw : 0.0));
     const double sc = (nn > drop * n0 && nn > 0.0) ? 1.0 / nn : 0.0;
-    if (cv) rows[w * stride + lane] = aw * sc;
+    if (cv) rows[w * STRIDE + lane] = aw * sc;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
@@ -702,26 +707,31 @@ __device__ __forceinline__ void setup_env(
       wsw[D::W_WR + p] = sWE[w * WEST + NV + 1 + c];
       wsw[D::W_WL + p] = sWA[w * WAST + NY1P + c];
     }
+    STAMP_END(9);
+    STAMP_BEGIN();
     // 4. T: an orthonormal basis of the y space whose first r' columns are Q's (nonzero) rows and
     //    the rest span their null space (Gram-Schmidt of [Q; I]).  The interior point and the
     //    refinement solve their Newton systems in y^ = T'y with the rows' coordinates pinned:
     //    the rows hold exactly, and nothing of the Hessian's curvature along them enters the
     //    factorisation.  X^ = X'T replaces X, so [Hr | g] below come out in these
     //    coordinates.
+    // (rows at an odd stride: the Gram-Schmidt's dot products read one row per lane, and at a stride
+    // of 32 doubles every lane's read hit the same LDS bank -- 58 % of the wheel assembly's time)
+    constexpr int TS = D::WTST;
     double* sWT = sm + D::O_WT;
     for (int p = lane; p < (NW + NY) * NY; p += kWave) {
       const int w = p / NY, c = p % NY;
-      sWT[p] = (w < NW) ? sWA[w * WAST + c] : ((c == w - NW) ? 1.0 : 0.0);
+      sWT[w * TS + c] = (w < NW) ? sWA[w * WAST + c] : ((c == w - NW) ? 1.0 : 0.0);
     }
     wave_sync();
-    wave_mgs_lds(sWT, NW + NY, NY, NY, NY, lane, 1e-9, sWE);   // (sWE: copied out above, free)
+    wave_mgs_lds<NW + NY, TS, NY, NY>(sWT, lane, 1e-9, sWE);   // (sWE: copied out above, free)
     wave_sync();
     int kept = 0;
     for (int w = 0; w < NW + NY; ++w) {
-      const double a = lane < NY ? sWT[w * NY + lane] : 0.0;
+      const double a = lane < NY ? sWT[w * TS + lane] : 0.0;
       if (wave_sum(a * a) > 0.0) {   // wave-uniform
         if (kept < NY) {
-          if (lane < NY) sWT[kept * NY + lane] = a;   // in place: kept <= w
+          if (lane < NY) sWT[kept * TS + lane] = a;   // in place: kept <= w
           if (lane == 0) wsw[D::W_PIN + kept] = (w < NW) ? static_cast<double>(w) : -1.0;
         }
         ++kept;
@@ -729,20 +739,22 @@ __device__ __forceinline__ void setup_env(
       wave_sync();
     }
     for (int k = kept; k < NY; ++k) {   // (never in practice: a column short -> pinned at zero)
-      if (lane < NY) sWT[k * NY + lane] = 0.0;
+      if (lane < NY) sWT[k * TS + lane] = 0.0;
       if (lane == 0) wsw[D::W_PIN + k] = -2.0;
     }
     wave_sync();
     for (int p = lane; p < NY * NY; p += kWave) {
       const int i = p / NY, k = p % NY;
-      wsw[D::W_T + p] = sWT[k * NY + i];   // T[i][k]
+      wsw[D::W_T + p] = sWT[k * TS + i];   // T[i][k]
     }
+    STAMP_END(10);
+    STAMP_BEGIN();
     // X^ = X'T (y columns; the affine column stays), staged in sWE (free now)
     for (int p = lane; p < NV * NY; p += kWave) {
       const int j = p / NY, k = p % NY;
       double v = 0.0;
 #pragma unroll 8
-      for (int i = 0; i < NY; ++i) v = fma(sX[j * NY1P + i], sWT[k * NY + i], v);
+      for (int i = 0; i < NY; ++i) v = fma(sX[j * NY1P + i], sWT[k * TS + i], v);
       sWE[p] = v;
     }
     wave_sync();
@@ -843,7 +855,7 @@ __device__ __forceinline__ void setup_env(
               for (int i = 0; i < NY; ++i) {
                 const int ki = (i >= NU) ? (i - NU) / 3 : 0;
                 const double wi = (i < NU) ? wu2 : (sMask[ki] == 0.0 ? 1.0 : wr2);
-                wab = fma(wi * sT[a * NY + i], sT[b * NY + i], wab);
+                wab = fma(wi * sT[a * D::WTST + i], sT[b * D::WTST + i], wab);
               }
               v += wab;
               wsv[D::W_HR + a * NY + b] = v;

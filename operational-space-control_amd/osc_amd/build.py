@@ -30,7 +30,7 @@ SOURCES = ["osc_ipm_go2.hip", "osc_ipm_walter.hip", "osc_ipm_wheels.hip", "osc_m
            "osc_setup.hip", "osc_gi.hip", "osc_dual.hip", "osc_kinematics.hip",
            "osc_producers.hip", "osc_api.hip", "osc_model.cpp", "osc_mjcf.cpp"]
 HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp", "osc_kin_device.hpp",
-           "osc_qpos.hpp"]
+           "osc_qpos.hpp", "osc_wave_sum.hpp"]
 # device-code units, for the static checks that read the generated assembly
 DEVICE_SOURCES = [s for s in SOURCES if s.endswith(".hip")]
 
