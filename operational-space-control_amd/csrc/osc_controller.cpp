@@ -384,7 +384,7 @@ Status OperationalSpaceController::fetch_outputs_locked() {
   if (info[0] != OSC_SOLVE_OK && info[0] != status_)
     std::cerr << "OperationalSpaceController: solve status " << info[0]
               << (info[0] == OSC_SOLVE_MAX_ITER     ? " (max_iter)"
-                  : info[0] == OSC_SOLVE_NUMERICAL  ? " (non-finite)"
+                  : info[0] == OSC_SOLVE_NUMERICAL  ? " (non-finite input or M not SPD)"
                   : info[0] == OSC_SOLVE_UNREFINED  ? " (unrefined)"
                                                     : "")
               << " after " << info[1] << " iterations; torques published as returned\n";
