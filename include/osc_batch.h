@@ -39,9 +39,10 @@
  *   x      [nenv][nv+nu+3nc]      (nullable) full design vector (dv, u, z) = get_solution()
  *   status [nenv]                 (nullable) OSC_SOLVE_* code per environment
  *   iters  [nenv]                 (nullable) interior-point iterations used; max_iter + k when
- *                                 the warm entries' cold fix-up pass re-solved the env (k its
- *                                 iterations); -k when the wheel rows' active-set fallback solved
- *                                 it in k steps (osc_batch_solve_ex / _warm_ex)
+ *                                 a cold fix-up pass re-solved the env (k its iterations: every
+ *                                 env the first pass leaves not OK, warm or cold entry -- see
+ *                                 OSC_SOLVE_UNREFINED); -k when the wheel rows' active-set
+ *                                 fallback solved it in k steps (osc_batch_solve_ex / _warm_ex)
  *
  * All batch pointers passed to osc_batch_solve are DEVICE pointers (HBM-resident); `stream` is
  * a hipStream_t (NULL = default stream).  The call is asynchronous with respect to the host.
@@ -85,13 +86,16 @@ typedef enum {
                                      forced off by osc_model_tuning.refine_max_move): the
                                      interior point's iterate is returned, accurate only to its
                                      stop (up to ~2e-2 normwise at eps_mu 1e-6
-                                     along the internal-force directions).  Cold entries return
-                                     it as is; the warm entries re-solve such an env cold to
-                                     mu <= 1e-12 first (then it is within ~1e-5 even if this
-                                     status remains).  Measured: none on the synthetic and
-                                     joint-state test batches; none in a census of 24 x 65,536
-                                     joint-state envs (round 5; ~1e-4 of the envs at joint
-                                     range 1.0 before the one-change refinement rounds)        */
+                                     along the internal-force directions).  Every entry
+                                     re-solves such an env (and a MAX_ITER or non-finite one)
+                                     cold to mu <= 1e-12 in a fix-up pass before returning
+                                     (round 5: cold solves too, in the same launch; not in the
+                                     lockstep-compaction and two-model kernels), and then it is
+                                     within ~1e-5 even if this status remains.  Measured: none
+                                     on the synthetic and joint-state test batches; 2 of 1.6 M
+                                     joint-state envs before that fix-up, none after (round 5
+                                     census, 48 x 65,536 envs; ~1e-4 of the envs at joint range
+                                     1.0 before the one-change refinement rounds)              */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C

@@ -294,7 +294,8 @@ void launch_t(LaunchArgs a, unsigned stages, const QposArgs* q) {
   // the workspace); it needs the per-env status, and so does a warm-started solve's cold fix-up
   // pass: the caller's array, else scratch at the end of the workspace.
   const bool fallback = D::WH;
-  if (a.status == nullptr && (a.warm != nullptr || fallback))
+  // (and so does the cold solve's fix-up pass in the interior-point launch, refinement fused)
+  if (a.status == nullptr && (a.warm != nullptr || fallback || a.model->refine))
     a.status = reinterpret_cast<int32_t*>(a.ws + static_cast<size_t>(D::WS) * a.nenv);
   launch_ipm<D>(a);
   if constexpr (D::WH) {

@@ -258,6 +258,8 @@ __device__ __forceinline__ void ipm_block(
   // to the dual kernel (W_SOL q, W_NU)
   const bool fixup = (flags & 1) != 0;
   const bool want_dual = (flags & 2) != 0;
+  // the refinement fused: a cold solve is followed by its own fix-up pass too (osc_ipm_kernel)
+  constexpr bool kFix = WARM || RF_ == kRfFused;
   constexpr int RF = RF_;
   constexpr bool REFINE = RF == kRfOnly;      // the refinement pass alone (no interior point)
   constexpr bool HRL = ipm_hrl<D, SMALL, RF>();
@@ -275,7 +277,7 @@ __device__ __forceinline__ void ipm_block(
   // Fix-up pass after a warm-started solve: only wavefronts holding an env that did not converge
   // run (cold, from the same workspace); only those envs' outputs are rewritten.
   bool write_out = valid;
-  if constexpr (WARM) {
+  if constexpr (kFix) {
     // (an env whose refinement found no KKT point, OSC_SOLVE_UNREFINED, too: the warm start can
     // leave the interior point's early stop with an active set the refinement cannot repair,
     // ~1 env in 4,096 x 10 joint-state ticks; the cold fix-up solve runs to mu <= 1e-12)
@@ -749,7 +751,7 @@ __device__ __forceinline__ void ipm_block(
     }
   };
   // interior-point stop (the warm fix-up pass is a rescue: its cold solve runs to mu <= 1e-12)
-  const double eps_run = (WARM && fixup) ? fmin(P->eps_mu, 1e-12) : P->eps_mu;
+  const double eps_run = (kFix && fixup) ? fmin(P->eps_mu, 1e-12) : P->eps_mu;
   if constexpr (REFINE) {
     // the interior point's result for this env (osc_ipm_kernel, W_SOL): y, and the active rows
     // as lambda > s with lambda = q > 0
@@ -1631,7 +1633,7 @@ __device__ __forceinline__ void ipm_block(
     }
     if (l == 0 && !REFINE) {
       if (gstatus) gstatus[env] = st;
-      if (giters) giters[env] = (WARM && fixup) ? P->max_iter + it_done : it_done;   // both passes
+      if (giters) giters[env] = (kFix && fixup) ? P->max_iter + it_done : it_done;   // both passes
     }
     if (WARM && !REFINE) {   // this tick's y and lambda for the next one (NaN: next tick cold)
       double* wo = gwarm + static_cast<size_t>(env) * D::WW;
@@ -1666,9 +1668,12 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : OSC_LARGE_WAVES) void osc_ipm_ke
   // mostly exit at once, cost 4.2 us of a 139 us Go2 4,096 warm tick
   ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                 gstatus, giters, gwarm, flags & 3, sm);
-  if constexpr (WARM) {
+  if constexpr (WARM || RF == kRfFused) {
     if (flags & 4) {   // (a second inlined body: a loop over both passes spilled 180 B per lane)
-      __threadfence();
+      // the statuses it reads are this wavefront's own stores: a workgroup-scope fence (their
+      // completion) is enough -- a device-scope __threadfence() wrote the L2 back in every
+      // wavefront, +15-18 % at 8,192 / 65,536 envs where two waves share each SIMD
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       ipm_block<D, SMALL, WARM, RF>(P, static_cast<int>(blockIdx.x), nenv, gmask, ws, gtau, gx,
                                     gstatus, giters, gwarm, (flags & 2) | 1, sm);
     }
@@ -1783,12 +1788,17 @@ void launch_ipm(const LaunchArgs& a) {
                            s, model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
       }
     } else if (warm == nullptr) {
+      // every env the interior point or the refinement leaves not OK (MAX_ITER, UNREFINED,
+      // non-finite) is re-solved cold to mu <= 1e-12 by its own wavefront in the same launch, as
+      // the warm entries do (round 5's census: ~1 such env per 600,000 joint-state envs; only
+      // the wavefronts holding one run the second pass)
+      const int fl = flags | 4;
       if (fused && small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, fl);
       else if (fused)
         hipLaunchKernelGGL((osc_ipm_kernel<D, false, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
-                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, fl);
       else if (small)
         hipLaunchKernelGGL((osc_ipm_kernel<D, true, false>), dim3(nb), dim3(kWave), 0, s,
                            model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr, flags);
