@@ -89,13 +89,13 @@ typedef enum {
                                      along the internal-force directions).  Every entry
                                      re-solves such an env (and a MAX_ITER or non-finite one)
                                      cold to mu <= 1e-12 in a fix-up pass before returning
-                                     (round 5: cold solves too, in the same launch; not in the
-                                     lockstep-compaction and two-model kernels), and then it is
-                                     within ~1e-5 even if this status remains.  Measured: none
-                                     on the synthetic and joint-state test batches; 2 of 1.6 M
-                                     joint-state envs before that fix-up, none after (round 5
-                                     census, 48 x 65,536 envs; ~1e-4 of the envs at joint range
-                                     1.0 before the one-change refinement rounds)              */
+                                     (round 5: cold solves too -- same launch, or a third one
+                                     after the lockstep compaction; not in the two-model kernels
+                                     of osc_batch_solve_multi), and then it is within ~1e-5
+                                     even if this status remains.  Measured: none on the
+                                     synthetic and joint-state test batches; 6 of 3.1 M
+                                     joint-state envs not OK before that fix-up (2 UNREFINED,
+                                     4 MAX_ITER), none after (round 5 census, 48 x 65,536)     */
 } osc_solve_status;
 
 /* Everything that defines the QP of one robot -- what autogen.py bakes into generated C

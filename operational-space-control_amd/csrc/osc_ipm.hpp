@@ -1075,9 +1075,13 @@ __device__ __forceinline__ void ipm_block(
     } else {
       // fraction to the boundary: 0.99 early, closer to 1 as mu -> 0 or when the affine step was
       // nearly full, never above 1 - 1e-5 (tools/ipm_model.py + tools/etatest.sh: -15% lockstep
-      // iterations vs a fixed 0.99; uncapped, a few envs stall at the boundary)
+      // iterations vs a fixed 0.99; uncapped, a few envs stall at the boundary).  The fix-up
+      // pass (an env the first pass left not OK) keeps 0.99: the envs of round 5's census that
+      // stalled at max_iter with the adaptive rule (~1 in 600,000 joint-state envs) converge in
+      // 15-20 iterations with it (numpy model of the kernel, tools/ipm_model.py)
       const double eta =
-          fmin(1.0 - 1e-5, fmax(0.99, fmax(1.0 - mu, 1.0 - 0.1 * (1.0 - a_aff))));
+          fixup ? 0.99
+                : fmin(1.0 - 1e-5, fmax(0.99, fmax(1.0 - mu, 1.0 - 0.1 * (1.0 - a_aff))));
       const double alpha = done ? 0.0 : fmin(1.0, eta * step);
       y0 = fma(alpha, dy0, y0);
       y1 = fma(alpha, dy1, y1);
@@ -1787,6 +1791,17 @@ void launch_ipm(const LaunchArgs& a) {
         hipLaunchKernelGGL((osc_ipm_compact_kernel<D, false, kCpResume>), dim3(nb), dim3(kWave), 0,
                            s, model->dparams, nenv, mask, ws, tau, x, status, iters, flags, pa);
       }
+      // the cold fix-up pass the one-launch solves run in their own launch (an env left not OK
+      // re-solved cold to mu <= 1e-12): here a third launch, whose wavefronts without such an
+      // env exit at once (round 5 census: 3 WaLTER envs in 1.6 M stalled at max_iter here)
+      if (small)
+        hipLaunchKernelGGL((osc_ipm_kernel<D, true, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr,
+                           (flags & 2) | 1);
+      else
+        hipLaunchKernelGGL((osc_ipm_kernel<D, false, false, kRfFused>), dim3(nb), dim3(kWave), 0, s,
+                           model->dparams, nenv, mask, ws, tau, x, status, iters, nullptr,
+                           (flags & 2) | 1);
     } else if (warm == nullptr) {
       // every env the interior point or the refinement leaves not OK (MAX_ITER, UNREFINED,
       // non-finite) is re-solved cold to mu <= 1e-12 by its own wavefront in the same launch, as

@@ -1,16 +1,21 @@
-"""Regenerate the oracle outputs of tests/golden/go2_unrefined_joint_states.npz (committed; re-run
-only to regenerate).
+"""Regenerate the oracle outputs of the joint-state regression fixtures under tests/golden/
+(committed; re-run only to regenerate).
 
     python tests/golden/make_joint_state_regressions.py
 
-PROVENANCE.  The inputs are the 12 Go2 environments that round 5's status census
-(tools/status_diag.py: 65,536-env joint-state batches, random_states seeds 11 / 13 / 14,
-joint_range 1.0, standing targets, all contacts on) found OSC_SOLVE_UNREFINED: their M, C, J, b
-as the GPU's kinematics kernel computed them (oracle/kinematics.py agrees to 1e-12), with the
-batch index (envs) and seed of each.  All 12 had the same cause -- the refinement's rounds cycled
-between active sets -- and returned torques up to 4e-3 (normwise) off.  The
-outputs (x, y, tau, cert) are the CPU oracle's exact optimum (oracle/qp_exact.py), KKT-certified,
-in make_golden.py's format, so test_oracle / test_gpu_parity pick the file up with the others.
+PROVENANCE.  The inputs are environments that round 5's status censuses (tools/status_diag.py:
+65,536-env joint-state batches, random_states seeds as in each file's `seed`, standing targets,
+all contacts on) found not OK, with their M, C, J, b as the GPU's kinematics kernel computed them
+(oracle/kinematics.py agrees to 1e-12) and their batch index (`envs`):
+* go2_unrefined_joint_states.npz -- 12 Go2 envs (seeds 11 / 13 / 14, joint_range 1.0)
+  OSC_SOLVE_UNREFINED: the refinement's rounds cycled between active sets;
+* go2_stalled_joint_states.npz -- 3 Go2 envs of the wider census (seeds 21 / 24 joint_range 1.0:
+  UNREFINED; seed 22, 0.5: MAX_ITER, the adaptive fraction-to-the-boundary rule stalling);
+* walter_stalled_joint_states.npz -- 3 WaLTER envs (seeds 23 / 24 range 1.5, 27 range 1.0:
+  MAX_ITER, the same stall).
+The outputs (x, y, tau, cert) are the CPU oracle's exact optimum (oracle/qp_exact.py),
+KKT-certified, in make_golden.py's format, so test_oracle / test_gpu_parity pick the files up with
+the others.
 """
 from __future__ import annotations
 
@@ -26,14 +31,17 @@ sys.path[:0] = [os.path.join(REPO, "oracle"), os.path.join(REPO, "operational-sp
 from osc_qp import build_qp, load_model, torque  # noqa: E402
 from qp_exact import certified, solve_exact  # noqa: E402
 
-PATH = os.path.join(HERE, "go2_unrefined_joint_states.npz")
+CASES = [("go2_unrefined_joint_states.npz", "unitree_go2"),
+         ("go2_stalled_joint_states.npz", "unitree_go2"),
+         ("walter_stalled_joint_states.npz", "walter_sr")]
 INPUTS = ("M", "C", "J", "b", "T", "mask", "envs", "seed")
 
 
-def main():
-    z = np.load(PATH)
+def make(name, robot):
+    path = os.path.join(HERE, name)
+    z = np.load(path)
     d = {k: z[k] for k in INPUTS}
-    model = load_model("unitree_go2")
+    model = load_model(robot)
     xs, ys, taus, certs = [], [], [], []
     for e in range(d["M"].shape[0]):
         args = [d[k][e] for k in ("M", "C", "J", "b", "T", "mask")]
@@ -43,11 +51,12 @@ def main():
         ys.append(sol.y)
         taus.append(torque(model, sol.x))
         certs.append([sol.cert[k] for k in ("stationarity", "primal", "dual", "complementarity")])
-    np.savez_compressed(PATH, **d, x=np.array(xs), y=np.array(ys), tau=np.array(taus),
-                        cert=np.array(certs), robot=np.array("unitree_go2"),
+    np.savez_compressed(path, **d, x=np.array(xs), y=np.array(ys), tau=np.array(taus),
+                        cert=np.array(certs), robot=np.array(robot),
                         scenario=np.array("joint_states"))
-    print(f"{os.path.basename(PATH)}: {len(xs)} envs, worst KKT residual {np.max(certs):.2e}")
+    print(f"{name}: {len(xs)} envs, worst KKT residual {np.max(certs):.2e}")
 
 
 if __name__ == "__main__":
-    main()
+    for case in CASES:
+        make(*case)

@@ -136,6 +136,34 @@ def test_joint_state_census_every_env_refined(gpu, seed):
     assert nw.max() <= NORM_ACH and el.max() <= ELEM_ACH, (nw.max(), el.max())
 
 
+@pytest.mark.parametrize("robot,seed,jr,fixture", [
+    ("unitree_go2", 22, 0.5, "go2_stalled_joint_states.npz"),
+    ("walter_sr", 23, 1.5, "walter_stalled_joint_states.npz"),
+])
+def test_joint_state_census_stalled_envs_fixed_up(gpu, robot, seed, jr, fixture):
+    """Round 5's wider census (48 x 65,536 joint-state envs): an env the adaptive fraction to the
+    boundary stalls at max_iter is re-solved cold (eta 0.99, mu <= 1e-12) by the fix-up pass -- in
+    the same launch (Go2), or in the third launch after the lockstep compaction's two (WaLTER at
+    65,536) -- so every env of these batches comes back OK, at the exact optimum."""
+    nenv = 65536
+    tree, kb, solver = _setup(robot)
+    qpos, qvel = random_states(tree, nenv, seed, joint_range=jr)
+    d = generate(robot, nenv, seed, "standing", "ones")
+    k = kb.compute(qpos, qvel, want_sites=False)
+    args = solver.prepare(k.M, k.C, k.J, k.b, d["T"], d["mask"])
+    out = solver.alloc_outputs(nenv)
+    solver.solve_into(out, *args)
+    torch.cuda.synchronize()
+    st = out.status.cpu().numpy()
+    assert (st == 0).all(), (np.bincount(st), np.nonzero(st)[0][:20])
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", fixture))
+    sel = g["seed"] == seed
+    envs = g["envs"][sel]
+    np.testing.assert_allclose(k.M.cpu().numpy()[envs], g["M"][sel], rtol=0, atol=1e-12)
+    nw, el = _rel_errors(out.tau.cpu().numpy()[envs], g["tau"][sel])
+    assert nw.max() <= NORM_ACH and el.max() <= ELEM_ACH, (nw.max(), el.max())
+
+
 @pytest.mark.parametrize("robot", ["unitree_go2", "walter_sr"])
 def test_joint_state_ticks(gpu, robot):
     """Ten consecutive 4,096-env ticks of a joint-space walk (hinge angles +-0.01 rad, velocities
