@@ -89,9 +89,10 @@ typedef enum {
                                      along the internal-force directions).  Every entry
                                      re-solves such an env (and a MAX_ITER or non-finite one)
                                      cold to mu <= 1e-12 in a fix-up pass before returning
-                                     (round 5: cold solves too -- same launch, or a third one
-                                     after the lockstep compaction; not in the two-model kernels
-                                     of osc_batch_solve_multi), and then it is within ~1e-5
+                                     (round 5: cold solves too -- same launch, a third one
+                                     after the lockstep compaction, a second one after the
+                                     two-model kernel of osc_batch_solve_multi), and then it is
+                                     within ~1e-5
                                      even if this status remains.  Measured: none on the
                                      synthetic and joint-state test batches; 6 of 3.1 M
                                      joint-state envs not OK before that fix-up (2 UNREFINED,

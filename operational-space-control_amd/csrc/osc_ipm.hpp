@@ -1715,17 +1715,19 @@ __global__ __launch_bounds__(kWave, SMALL ? 1 : 2) void osc_refine_kernel(
 // the first model's early finishers free (its iteration-count tail) -- two grids on two streams
 // instead split the SIMDs between the models and each pays its own tail.
 template <class DA, class DB, int RF = kRfNone>
-__global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, PairArgs B) {
+__global__ __launch_bounds__(kWave, 1) void osc_ipm_pair_kernel(PairArgs A, PairArgs B, int flags) {
   __shared__ __attribute__((aligned(16))) double
       sm[cmax(ipm_lds_doubles<DA, true, RF>(), ipm_lds_doubles<DB, true, RF>())];
   const int nbA = (A.nenv + kEnvPerWave - 1) / kEnvPerWave;
   const int blk = static_cast<int>(blockIdx.x);
+  // (flags bit 0: the cold fix-up pass over the envs left not OK, launched after the solve when
+  // refinement is fused -- a second launch: a second inlined body per model spills, launch_pair)
   if (blk < nbA)
     ipm_block<DA, true, false, RF>(A.P, blk, A.nenv, A.mask, A.ws, A.tau, A.x, A.status,
-                                       A.iters, nullptr, 0, sm);
+                                   A.iters, nullptr, flags & 1, sm);
   else
     ipm_block<DB, true, false, RF>(B.P, blk - nbA, B.nenv, B.mask, B.ws, B.tau, B.x,
-                                       B.status, B.iters, nullptr, 0, sm);
+                                   B.status, B.iters, nullptr, flags & 1, sm);
 }
 
 // ---- launch_ipm: the interior-point passes of one call (after the assembly) ----

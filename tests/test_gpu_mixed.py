@@ -122,3 +122,44 @@ def test_multi_rejects_bad_jobs(gpu):
     assert e.value.code == 1
     assert _lib.lib().osc_batch_solve_multi(None, 1, None) == 1
     assert _lib.lib().osc_batch_solve_multi(None, 0, None) == 0
+
+
+def test_multi_fixup_rescues_stalled_envs(gpu):
+    """The two-model kernels run the cold fix-up pass too (a second interior-point launch over the
+    envs the solve left not OK): the census's stalled and formerly unrefined joint-state envs
+    (tests/golden/*_joint_states.npz), solved as one Go2 + WaLTER call, all come back OK, bitwise
+    the solo solves (whose fix-up runs in the same launch) and at the fixtures' optimum."""
+    import os
+    from osc_amd.solver import OSCBatchSolver, solve_multi_into
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    keys = ("M", "C", "J", "b", "T", "mask")
+    sets = {"unitree_go2": ("go2_stalled_joint_states.npz", "go2_unrefined_joint_states.npz"),
+            "walter_sr": ("walter_stalled_joint_states.npz",)}
+    jobs, refs = [], []
+    for robot in ROBOTS:
+        gs = [np.load(os.path.join(gdir, f)) for f in sets[robot]]
+        d = {k: np.concatenate([g[k] for g in gs]) for k in keys + ("tau",)}
+        s = OSCBatchSolver(robot)
+        jobs.append((s, s.alloc_outputs(d["M"].shape[0], want_x=True),
+                     s.prepare(*(d[k] for k in keys))))
+        refs.append(d["tau"])
+    solo = _solo_sized(jobs)
+    solve_multi_into(jobs)
+    torch.cuda.synchronize()
+    for (s, out, _), (tau, x, st), ref in zip(jobs, solo, refs):
+        got = out.tau.cpu().numpy()
+        assert (out.status.cpu().numpy() == 0).all(), (s.robot, out.status.cpu().numpy())
+        assert (st == 0).all()
+        assert np.array_equal(got, tau) and np.array_equal(out.x.cpu().numpy(), x), s.robot
+        err = np.abs(got - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1.0)
+        assert err.max() <= NORM_TOL, (s.robot, err.max())
+
+
+def _solo_sized(jobs):
+    out = []
+    for s, o, inputs in jobs:
+        r = s.alloc_outputs(o.tau.shape[0], want_x=True)
+        s.solve_into(r, *inputs)
+        out.append(r)
+    torch.cuda.synchronize()
+    return [(r.tau.cpu().numpy(), r.x.cpu().numpy(), r.status.cpu().numpy()) for r in out]
