@@ -197,9 +197,14 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   int act = -1;         // lane j < q: row id of working row j
   double up = 0.0;      // lane j <= q: multipliers (j = q: the candidate's)
   double zi = 0.0;      // lane i: the primal step direction z
-  double rj = 0.0;      // lane j < q: R^-1 d[:q]
+  double rj = 0.0;      // lane j in [qe, q): R^-1 d[:q]
+  int qe = kWave;       // working equality rows (positions [0, qe), never dropped), once all are in
   // d = J'c (lane j -> sd), z = J[:, q:] d[q:] (lane i), r = R^-1 d[:q] (lane j).  c: a dense
-  // equality row in sc, or one-sided row p (<= 3 nonzeros: only those rows of J are read)
+  // equality row in sc, or one-sided row p (<= 3 nonzeros: only those rows of J are read).
+  // r is only back-substituted down to position qe: the equality rows' multipliers are never read
+  // (no sign test, no drop, not returned), and R's triangle puts them after the one-sided rows'
+  // entries in the back substitution -- so the equality phase skips it, and the one-sided steps
+  // run q - qe of its serial steps instead of q (x, tau and the working set unchanged, bitwise)
   auto directions = [&](int p) {
     if (lane < NX) {
       double t = 0.0;
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     }
     double dv = lane < q ? sd[lane] : 0.0;
     rj = 0.0;
-    for (int jj = q - 1; jj >= 0; --jj) {   // back substitution, column-oriented
+    for (int jj = q - 1; jj >= qe; --jj) {   // back substitution, column-oriented
       const double v = readlane_d(dv, jj) * sRi[jj];
       if (lane == jj) rj = v;
       if (lane < jj) dv = fma(-sR[lane * NXP + jj], v, dv);
@@ -362,13 +367,13 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     const double t = (sEb[k] - cx) / zc;
     if (!isfinite(t)) { ok = false; break; }
     xi = fma(t, zi, xi);
-    if (lane < q) up = fma(-t, rj, up);
-    if (lane == q) { up = t; act = k; }
+    if (lane == q) { up = t; act = k; }   // (the other equality rows' multipliers: not kept)
     GI_T0();
     add_row();
     GI_T1(1);
     ++q;
   }
+  qe = q;
   if (lane < NX) sx[lane] = xi;
   __syncthreads();
   // ---- one-sided rows ----
@@ -410,6 +415,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       directions(p);
       GI_T1(3);
       // partial step: the working one-sided row whose multiplier reaches 0 first
+      // (rmax: over the one-sided working rows -- the equality rows' rj are not computed)
       const double rmax = 1.0 + wmax(lane < q ? fabs(rj) : 0.0);
       double t1 = INFINITY;
       int kd = lane;

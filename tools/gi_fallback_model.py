@@ -140,7 +140,10 @@ def gi_full(H, f, cs, bs, eqs, max_steps=400):
             z = Jm[:, q:] @ d[q:]
             r = np.linalg.solve(R[:q, :q], d[:q]) if q else np.zeros(0)
             t1, kdrop = np.inf, -1
-            rmax = 1.0 + (np.abs(r).max() if q else 0.0)
+            # (the kernel's scale: the one-sided working rows' entries only -- it never
+            # back-substitutes the equality rows' part of r, round 5)
+            ineq = np.array([a >= neq for a in act], bool)
+            rmax = 1.0 + (np.abs(r[ineq]).max() if ineq.any() else 0.0)
             for j in range(q):
                 if act[j] >= neq and r[j] > 1e-14 * rmax and up[j] / r[j] < t1:
                     t1, kdrop = up[j] / r[j], j

@@ -7,6 +7,7 @@ exact oracle.  One parameterised tool in place of round 3's wheel_* one-offs.
 (--brief: the per-tick summary lines only, no oracle solves; --dump=OUT.npz: x, y, status and the
 inputs of every env not certified, for a CPU look at its certificate)
 """
+import hashlib
 import json
 import os
 import sys
@@ -81,7 +82,9 @@ def main():
                "status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
                "ok_uncertified": int(((st == 0) & ~good).sum()), "worst_cert_of_ok": worst,
                "iters_mean": float(out.iters.float().mean().item()),
-               "iters_max": int(out.iters.max().item()), "ms": ms}
+               "iters_max": int(out.iters.max().item()), "ms": ms,
+               "tau_x_sha": hashlib.sha1(out.tau.cpu().numpy().tobytes() +
+                                         out.x.cpu().numpy().tobytes()).hexdigest()[:16]}
         print(json.dumps(row), flush=True)
         tau = out.tau.cpu().numpy()
         it = out.iters.cpu().numpy()
