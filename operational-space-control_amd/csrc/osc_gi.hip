@@ -43,6 +43,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   __shared__ double sJ[NX * NXP];             // J (row i at i * NXP); first the Cholesky factor
   __shared__ double sR[NX * NXP];             // R, upper triangular (row i at i * NXP)
   __shared__ double sx[NX], sc[NX], sd[NX], sgc[NX], sgs[NX], sRi[NX];   // sRi: 1 / R[j][j]
+  __shared__ double2 sCS[NX];                 // add_row's rotations (c, s)
   const double* wenv = ws + static_cast<size_t>(env) * D::WS;
   // the raw rows, as the setup kernel copied them into this env's workspace block: M, C, the
   // contact rows of J (Jc, 3 NC x NV) and of b (bc), the wheel directions
@@ -193,6 +194,17 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   const double jscale = sqrt(wmax(rn));
   __syncthreads();
 
+#ifdef OSC_GI_PROFILE
+  unsigned long long tp[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, t1_ = 0, ta = 0, tb = 0;
+  int ndrop = 0, nadd = 0;
+#define GI_T0() asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory")
+#define GI_T1(k) do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory"); tp[k] += t1_ - t0; } while (0)
+#define GI_TA(v) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
+#else
+#define GI_TA(v) do {} while (0)
+#define GI_T0() do {} while (0)
+#define GI_T1(k) do {} while (0)
+#endif
   int q = 0;            // working rows
   int act = -1;         // lane j < q: row id of working row j
   double up = 0.0;      // lane j <= q: multipliers (j = q: the candidate's)
@@ -206,6 +218,9 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   // entries in the back substitution -- so the equality phase skips it, and the one-sided steps
   // run q - qe of its serial steps instead of q (x, tau and the working set unchanged, bitwise)
   auto directions = [&](int p) {
+#ifdef OSC_GI_PROFILE
+    GI_TA(ta);
+#endif
     if (lane < NX) {
       double t = 0.0;
       if (p < 0) {
@@ -228,6 +243,11 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       sd[lane] = t;
     }
     __syncthreads();
+#ifdef OSC_GI_PROFILE
+    GI_TA(tb);
+    tp[8] += tb - ta;
+    GI_TA(ta);
+#endif
     zi = 0.0;
     if (lane < NX) {
       double z1 = 0.0;
@@ -239,6 +259,11 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       if (j < NX) zi = fma(sJ[lane * NXP + j], sd[j], zi);
       zi += z1;
     }
+#ifdef OSC_GI_PROFILE
+    GI_TA(tb);
+    tp[9] += tb - ta;
+    GI_TA(ta);
+#endif
     double dv = lane < q ? sd[lane] : 0.0;
     rj = 0.0;
     for (int jj = q - 1; jj >= qe; --jj) {   // back substitution, column-oriented
@@ -246,12 +271,19 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       if (lane == jj) rj = v;
       if (lane < jj) dv = fma(-sR[lane * NXP + jj], v, dv);
     }
+#ifdef OSC_GI_PROFILE
+    GI_TA(tb);
+    tp[10] += tb - ta;
+#endif
   };
   // c joins the working set at position q: the rotations (j-1, j), j = NX-1 .. q+1, that fold
   // d[q+1:] into d[q] (J's columns follow); rotation j meets (d[j-1], ||d[j:]||) -- d[NX-1] itself,
   // signed, for the first -- so every (c, s) follows from d's suffix sums of squares, one wave
   // scan instead of a chain of NX - q dependent rotations.  R's column q = d[:q+1].
   auto add_row = [&]() {
+#ifdef OSC_GI_PROFILE
+    GI_TA(ta);
+#endif
     const double dl = lane < NX ? sd[lane] : 0.0;
     double ssq = (lane >= q && lane < NX) ? dl * dl : 0.0;
     for (int o = 1; o < kWave; o <<= 1) {   // suffix sums S_j = sum_{k >= j} d_k^2
@@ -260,34 +292,43 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     }
     const double sn = __shfl_down(ssq, 1, kWave);            // S_{j+1} on lane j
     const double dnext = __shfl_down(dl, 1, kWave);          // d_{j+1} on lane j
-    if (lane >= q && lane < NX - 1) {   // lane j - 1 holds rotation j's (c, s)
+    if (lane < NX - 1) {   // lane j - 1 holds rotation j's (c, s); rotations j <= q: identity
       const double rr = sqrt(ssq);
       double c = 1.0, sv = 0.0;
-      if (rr > 0.0) {
+      if (lane >= q && rr > 0.0) {
         c = dl / rr;
         sv = (lane + 1 == NX - 1 ? dnext : sqrt(sn)) / rr;
       }
-      sgc[lane + 1] = c;
-      sgs[lane + 1] = sv;
+      sCS[lane + 1] = make_double2(c, sv);
     }
     const double dq = __shfl(q < NX - 1 ? sqrt(ssq) : dl, q, kWave);
     __syncthreads();
+#ifdef OSC_GI_PROFILE
+    GI_TA(tb);
+    tp[7] += tb - ta;
+    GI_TA(ta);
+#endif
     if (lane < NX) {
       double row[NX];
 #pragma unroll
       for (int c = 0; c < NX; ++c) row[c] = sJ[lane * NXP + c];
+      // (every rotation applied, the identity ones too: no branch per rotation, so the (c, s)
+      // reads issue ahead of the chain; c * a + s * b with (1, 0) returns a, bitwise)
 #pragma unroll
       for (int j = NX - 1; j >= 1; --j) {
-        if (j > q) {
-          const double c = sgc[j], sv = sgs[j];
-          const double a = row[j - 1], b = row[j];
-          row[j - 1] = c * a + sv * b;
-          row[j] = -sv * a + c * b;
-        }
+        const double2 cs = sCS[j];
+        const double c = cs.x, sv = cs.y;
+        const double a = row[j - 1], b = row[j];
+        row[j - 1] = c * a + sv * b;
+        row[j] = -sv * a + c * b;
       }
 #pragma unroll
       for (int c = 0; c < NX; ++c) sJ[lane * NXP + c] = row[c];
     }
+#ifdef OSC_GI_PROFILE
+    GI_TA(tb);
+    tp[6] += tb - ta;
+#endif
     if (lane < q) sR[lane * NXP + q] = dl;
     if (lane == q) {
       sR[q * NXP + q] = dq;
@@ -344,15 +385,6 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
 
   bool ok = true;
   int steps = 0;
-#ifdef OSC_GI_PROFILE
-  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, t0 = 0, t1_ = 0;
-  int ndrop = 0, nadd = 0;
-#define GI_T0() asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory")
-#define GI_T1(k) do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory"); tp[k] += t1_ - t0; } while (0)
-#else
-#define GI_T0() do {} while (0)
-#define GI_T1(k) do {} while (0)
-#endif
   // ---- equality rows: always in, never dropped; a row dependent on those already in skipped ----
   for (int k = 0; k < neq && ok; ++k) {
     const double ck = lane < NX ? sE[k * NXP + lane] : 0.0;
@@ -454,8 +486,8 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   }
 #ifdef OSC_GI_PROFILE
   if (lane == 0)
-    printf("gi env %d ok %d steps %d neq %d q %d adds %d drops %d cyc eqdir %llu eqadd %llu scan %llu dir %llu add %llu drop %llu\n",
-           env, ok ? 1 : 0, steps, neq, q, nadd, ndrop, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]);
+    printf("gi env %d ok %d steps %d neq %d q %d adds %d drops %d cyc eqdir %llu eqadd %llu scan %llu dir %llu add %llu drop %llu rot %llu scan_cs %llu jc %llu z %llu bs %llu\n",
+           env, ok ? 1 : 0, steps, neq, q, nadd, ndrop, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7], tp[8], tp[9], tp[10]);
 #endif
   if (!ok) return;
   // ---- certify: every equality row held, every one-sided row feasible, and every

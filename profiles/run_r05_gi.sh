@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
-O=gpurun_out/r05gi
+O=gpurun_out/${GI_OUT:-r05gi}
 mkdir -p $O
 for seed in 91 92; do
 for lib in ab_old/libosc_batch.so libosc_batch.so; do
