@@ -883,8 +883,13 @@ __device__ __forceinline__ void setup_env(
 
 // The assembly grid maps block b to env b: an XCD-aware order that put each env's assembly on
 // the XCD of its interior-point block measured no change (Go2 4,096 0.1819 vs 0.1815 ms).
+// (waves per SIMD of the launch bound; -DOSC_SETUP_WPS=3 for A/B builds: 168 VGPRs + 436 B of
+// spills, Go2 4,096 0.166 -> 0.226 ms per solve, profiles/r05/r05wps_*)
+#ifndef OSC_SETUP_WPS
+#define OSC_SETUP_WPS 2
+#endif
 template <class D, bool LEAN = false>
-__global__ __launch_bounds__(kWave, 2) void osc_setup_kernel(
+__global__ __launch_bounds__(kWave, OSC_SETUP_WPS) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
