@@ -38,6 +38,13 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   __shared__ double sr[NC * 3];   // per contact: r_k
   const int env = static_cast<int>(blockIdx.x), lane = static_cast<int>(threadIdx.x);
   if (env >= nenv) return;
+#ifdef OSC_DUAL_PROFILE   // per-phase clocks of one wave (diagnostic build, printf per env)
+  unsigned long long dp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dt0 = 0, dt1 = 0;
+#define DU_T(k) do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dt1)::"memory"); dp[k] += dt1 - dt0; dt0 = dt1; } while (0)
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dt0)::"memory");
+#else
+#define DU_T(k) do {} while (0)
+#endif
   const double* w = ws + static_cast<size_t>(env) * D::WS;
   const double* x = gx + static_cast<size_t>(env) * NX;
   const double* J = gJ + static_cast<size_t>(env) * S * NV;
@@ -62,6 +69,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     if (lane >= k && lane < NV) sL[lane * NV + k] = (lane == k) ? dk : t / dk;
     __syncthreads();
   }
+  DU_T(0);
   // L L' v = b in place (one lane, serial)
   auto chol_solve = [&](double* v) {
     for (int i = 0; i < NV; ++i) {
@@ -120,6 +128,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
       else sJN0[kc] = a;
     }
     __syncthreads();
+    DU_T(1);
     if (lane == 0) {
       const double wu = 2.0 * (P->w_torque + P->w_reg), wz = 2.0 * P->w_reg, mu = P->mu;
       int n = 0;
@@ -196,6 +205,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
       snrow = n;
     }
     __syncthreads();
+    DU_T(2);
     // the basic least-squares solution by Householder QR with column pivoting (rank: |R_jj| >
     // 1e-10 |R_00|; the dependent rows' multipliers are zero).  (Normal equations do not do: the
     // rows that fix dv need multipliers up to ~1e6 along directions whose singular values are
@@ -271,6 +281,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     }
   }
   __syncthreads();
+  DU_T(3);
   if (lane < NV) {   // g_x = g0 (+ E' nu_w)
     double a = sg[lane];
     if constexpr (D::WH) {
@@ -303,6 +314,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     }
   }
   __syncthreads();
+  DU_T(4);
   if (lane < NC) {   // contact `lane`: r_k, then its rows' multipliers
     const int k = lane;
     const double wz = 2.0 * P->w_reg, mu = P->mu;
@@ -316,83 +328,85 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     }
     double q[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (mask[k] != 0.0) {
-      // rows g_i' f <= h_i: pyramid (sx, sy, -mu) <= 0, -fz <= -lb, fz <= ub
+      // rows g_i' f <= h_i: pyramid (sx, sy, -mu) <= 0, -fz <= -lb, fz <= ub; the normals as
+      // closed forms of the row index (no row arrays: a runtime-indexed array lives in scratch,
+      // and the subset loop below indexes by the subset's rows)
       const double ub = P->z_ub[2] * mask[k], lb = P->z_lb[2] * mask[k];
-      double g[6][3], h[6];
-      for (int i = 0; i < 4; ++i) {
-        g[i][0] = (i & 1) ? -1.0 : 1.0;
-        g[i][1] = (i >= 2) ? -1.0 : 1.0;
-        g[i][2] = -mu;
-        h[i] = 0.0;
-      }
-      g[4][0] = g[4][1] = 0.0; g[4][2] = -1.0; h[4] = -lb;
-      g[5][0] = g[5][1] = 0.0; g[5][2] = 1.0;  h[5] = ub;
+      auto gco = [&](int i, int c) -> double {
+        if (i < 4) return c == 0 ? ((i & 1) ? -1.0 : 1.0) : (c == 1 ? ((i >= 2) ? -1.0 : 1.0) : -mu);
+        return c == 2 ? (i == 4 ? -1.0 : 1.0) : 0.0;
+      };
       const double tol = 1e-8 * (1.0 + fmax(fabs(f[0]), fmax(fabs(f[1]), fabs(f[2]))));
       int act = 0;
+#pragma unroll
       for (int i = 0; i < 6; ++i) {
-        const double gi = g[i][0] * f[0] + g[i][1] * f[1] + g[i][2] * f[2] - h[i];
-        const bool finite = (i < 4) || fabs(h[i]) < P->inf_thresh;
+        const double h = i < 4 ? 0.0 : (i == 4 ? -lb : ub);
+        const double gi = gco(i, 0) * f[0] + gco(i, 1) * f[1] + gco(i, 2) * f[2] - h;
+        const bool finite = (i < 4) || fabs(h) < P->inf_thresh;
         if (finite && gi >= -tol) act |= 1 << i;
       }
-      // min |r + G_S' m| over m >= 0, S a subset of the active rows with |S| <= 3
+      // min |r + G_S' m| over m >= 0, S a subset of the active rows with |S| <= 3 (Caratheodory):
+      // per subset the 3 x 3 Gram system (G_S G_S') m = -G_S r by LDL^T (symmetric positive
+      // semi-definite; a pivot under 1e-12 marks a dependent subset, skipped), unused slots as
+      // identity rows -- all in registers
       double best = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
       int bestS = 0;
-      double bm[3] = {0.0, 0.0, 0.0};
+      double bm0 = 0.0, bm1 = 0.0, bm2 = 0.0;
+#pragma unroll 1
       for (int S = 1; S < 64; ++S) {
-        if ((S & act) != S || __builtin_popcount(S) > 3) continue;
-        int id[3], n = 0;
-        for (int i = 0; i < 6; ++i)
-          if (S >> i & 1) id[n++] = i;
-        double A[3][3], bb[3];   // (G_S G_S') m = -G_S r
-        for (int a = 0; a < n; ++a) {
-          bb[a] = -(g[id[a]][0] * r[0] + g[id[a]][1] * r[1] + g[id[a]][2] * r[2]);
-          for (int c = 0; c < n; ++c)
-            A[a][c] = g[id[a]][0] * g[id[c]][0] + g[id[a]][1] * g[id[c]][1] + g[id[a]][2] * g[id[c]][2];
-        }
-        bool ok = true;   // Gaussian elimination with partial pivoting, n <= 3
-        for (int c = 0; c < n && ok; ++c) {
-          int p = c;
-          for (int a = c + 1; a < n; ++a)
-            if (fabs(A[a][c]) > fabs(A[p][c])) p = a;
-          if (fabs(A[p][c]) < 1e-12) { ok = false; break; }
-          if (p != c) {
-            for (int e = 0; e < n; ++e) { const double t = A[c][e]; A[c][e] = A[p][e]; A[p][e] = t; }
-            const double t = bb[c]; bb[c] = bb[p]; bb[p] = t;
-          }
-          for (int a = c + 1; a < n; ++a) {
-            const double fct = A[a][c] / A[c][c];
-            for (int e = c; e < n; ++e) A[a][e] -= fct * A[c][e];
-            bb[a] -= fct * bb[c];
-          }
-        }
-        if (!ok) continue;
-        double m[3];
-        for (int a = n - 1; a >= 0; --a) {
-          double t = bb[a];
-          for (int e = a + 1; e < n; ++e) t -= A[a][e] * m[e];
-          m[a] = t / A[a][a];
-        }
-        bool nonneg = true;
-        for (int a = 0; a < n; ++a) nonneg = nonneg && m[a] >= 0.0;
-        if (!nonneg) continue;
+        const int n = __builtin_popcount(S);
+        if ((S & act) != S || n > 3) continue;
+        const int S1 = S & (S - 1), S2 = S1 & (S1 - 1);
+        const int i0 = __builtin_ctz(S), i1 = S1 ? __builtin_ctz(S1) : 0, i2 = S2 ? __builtin_ctz(S2) : 0;
+        const double a0 = gco(i0, 0), a1 = gco(i0, 1), a2 = gco(i0, 2);
+        const double b0 = n > 1 ? gco(i1, 0) : 0.0, b1 = n > 1 ? gco(i1, 1) : 0.0,
+                     b2 = n > 1 ? gco(i1, 2) : 0.0;
+        const double c0 = n > 2 ? gco(i2, 0) : 0.0, c1 = n > 2 ? gco(i2, 1) : 0.0,
+                     c2 = n > 2 ? gco(i2, 2) : 0.0;
+        const double A00 = a0 * a0 + a1 * a1 + a2 * a2, A01 = a0 * b0 + a1 * b1 + a2 * b2,
+                     A02 = a0 * c0 + a1 * c1 + a2 * c2;
+        const double A11 = n > 1 ? b0 * b0 + b1 * b1 + b2 * b2 : 1.0,
+                     A12 = b0 * c0 + b1 * c1 + b2 * c2;
+        const double A22 = n > 2 ? c0 * c0 + c1 * c1 + c2 * c2 : 1.0;
+        const double r0 = -(a0 * r[0] + a1 * r[1] + a2 * r[2]);
+        const double r1 = -(b0 * r[0] + b1 * r[1] + b2 * r[2]);
+        const double r2 = -(c0 * r[0] + c1 * r[1] + c2 * r[2]);
+        const double d0 = A00;
+        if (!(d0 >= 1e-12)) continue;
+        const double l10 = A01 / d0, l20 = A02 / d0;
+        const double d1 = A11 - l10 * A01;
+        if (!(d1 >= 1e-12)) continue;
+        const double l21 = (A12 - l20 * A01) / d1;
+        const double d2 = A22 - l20 * A02 - l21 * l21 * d1;
+        if (!(d2 >= 1e-12)) continue;
+        const double y0 = r0, y1 = r1 - l10 * y0, y2 = r2 - l20 * y0 - l21 * y1;
+        const double m2 = y2 / d2, m1 = y1 / d1 - l21 * m2, m0 = y0 / d0 - l10 * m1 - l20 * m2;
+        if (!(m0 >= 0.0 && m1 >= 0.0 && m2 >= 0.0)) continue;
         double res = 0.0;
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
-          double t = r[c];
-          for (int a = 0; a < n; ++a) t += m[a] * g[id[a]][c];
+          const double t = r[c] + m0 * (c == 0 ? a0 : c == 1 ? a1 : a2) +
+                           m1 * (c == 0 ? b0 : c == 1 ? b1 : b2) + m2 * (c == 0 ? c0 : c == 1 ? c1 : c2);
           res += t * t;
         }
         if (res < best * (1.0 - 1e-12)) {
           best = res;
           bestS = S;
-          for (int a = 0; a < 3; ++a) bm[a] = a < n ? m[a] : 0.0;
+          bm0 = m0;
+          bm1 = m1;
+          bm2 = m2;
         }
       }
-      for (int i = 0, a = 0; i < 6; ++i)
-        if (bestS >> i & 1) q[i] = bm[a++];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int a = __builtin_popcount(bestS & ((1 << i) - 1));
+        if (bestS >> i & 1) q[i] = a == 0 ? bm0 : (a == 1 ? bm1 : bm2);
+      }
     }
     for (int i = 0; i < 6; ++i) sq[6 * k + i] = q[i];
   }
   __syncthreads();
+  DU_T(5);
   double* y = gy + static_cast<size_t>(env) * NROW;
   const double wu = 2.0 * (P->w_torque + P->w_reg);
   for (int r = lane; r < NROW; r += kWave) {
@@ -416,6 +430,12 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
     }
     y[r] = v;
   }
+#ifdef OSC_DUAL_PROFILE
+  DU_T(6);
+  if (lane == 0 && env % 256 == 0)
+    printf("dual env %d cyc chol %llu wrows %llu lsrows %llu qr %llu nu %llu nnls %llu out %llu\n", env,
+           dp[0], dp[1], dp[2], dp[3], dp[4], dp[5], dp[6]);
+#endif
 }
 
 template <class D>
