@@ -2,6 +2,7 @@
 // osc_solve_extras.y): OsqpSolver::dual_solution, unitree_go2/operational_space_controller.h:
 // 534-535.
 #include "osc_internal.hpp"
+#include "osc_wave_sum.hpp"
 
 namespace osc {
 
@@ -145,49 +146,73 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
         if (mask[k] == 0.0) continue;
         const double f0 = x[NV + NU + 3 * k], f1 = x[NV + NU + 3 * k + 1], f2 = x[NV + NU + 3 * k + 2];
         const double tol = 1e-9 * (1.0 + fmax(fabs(f0), fmax(fabs(f1), fabs(f2))));
-        double q[3][3];   // orthonormal basis of the active normals' span (Gram-Schmidt)
+        // orthonormal basis of the active normals' span (Gram-Schmidt), then its complement; the
+        // slot loops run over compile-time slots with the runtime count as a predicate (runtime-
+        // indexed arrays would live in scratch)
+        double q[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
         int rk = 0;
         const double ub = P->z_ub[2] * mask[k], lb = P->z_lb[2] * mask[k];
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
           double g[3];
           double gap;
+          bool have = true;
           if (i < 4) {
             g[0] = (i & 1) ? -1.0 : 1.0; g[1] = (i >= 2) ? -1.0 : 1.0; g[2] = -mu;
             gap = -(g[0] * f0 + g[1] * f1 + g[2] * f2);
           } else if (i == 4) {
-            if (!(fabs(lb) < P->inf_thresh)) continue;
+            have = fabs(lb) < P->inf_thresh;
             g[0] = g[1] = 0.0; g[2] = -1.0; gap = f2 - lb;
           } else {
-            if (!(fabs(ub) < P->inf_thresh)) continue;
+            have = fabs(ub) < P->inf_thresh;
             g[0] = g[1] = 0.0; g[2] = 1.0; gap = ub - f2;
           }
-          if (gap > tol || rk == 3) continue;
-          for (int a = 0; a < rk; ++a) {
-            const double d = g[0] * q[a][0] + g[1] * q[a][1] + g[2] * q[a][2];
-            for (int c = 0; c < 3; ++c) g[c] -= d * q[a][c];
+          if (!have || gap > tol || rk == 3) continue;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            if (a < rk) {
+              const double d = g[0] * q[a][0] + g[1] * q[a][1] + g[2] * q[a][2];
+              for (int c = 0; c < 3; ++c) g[c] -= d * q[a][c];
+            }
           }
           const double nn = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
           if (nn > 1e-6) {
-            for (int c = 0; c < 3; ++c) q[rk][c] = g[c] / nn;
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+              if (a == rk)
+                for (int c = 0; c < 3; ++c) q[a][c] = g[c] / nn;
             ++rk;
           }
         }
         // complement: e_c orthogonalised against the span and the complement vectors so far
         int nc = 0;
-        double pc[3][3];
-        for (int c = 0; c < 3 && rk + nc < 3; ++c) {
+        double pc[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (rk + nc >= 3) break;
           double v[3] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0};
-          for (int a = 0; a < rk; ++a) {
-            const double d = v[0] * q[a][0] + v[1] * q[a][1] + v[2] * q[a][2];
-            for (int e = 0; e < 3; ++e) v[e] -= d * q[a][e];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            if (a < rk) {
+              const double d = v[0] * q[a][0] + v[1] * q[a][1] + v[2] * q[a][2];
+              for (int e = 0; e < 3; ++e) v[e] -= d * q[a][e];
+            }
           }
-          for (int a = 0; a < nc; ++a) {
-            const double d = v[0] * pc[a][0] + v[1] * pc[a][1] + v[2] * pc[a][2];
-            for (int e = 0; e < 3; ++e) v[e] -= d * pc[a][e];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            if (a < nc) {
+              const double d = v[0] * pc[a][0] + v[1] * pc[a][1] + v[2] * pc[a][2];
+              for (int e = 0; e < 3; ++e) v[e] -= d * pc[a][e];
+            }
           }
           const double nn = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
           if (nn < 0.5) continue;
-          for (int e = 0; e < 3; ++e) pc[nc][e] = v[e] / nn;
+          double pn[3];
+          for (int e = 0; e < 3; ++e) pn[e] = v[e] / nn;
+#pragma unroll
+          for (int a = 0; a < 3; ++a)
+            if (a == nc)
+              for (int e = 0; e < 3; ++e) pc[a][e] = pn[e];
           // p' r_k = 0 with r_k = wz f - Jc_k' (nu0 - W nu_w)
           double rhs = 0.0;
           double* row = sA + n * NW;   // (built in place)
@@ -195,8 +220,8 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
           for (int cc = 0; cc < 3; ++cc) {
             const double jn0 = sJN0[3 * k + cc];
             const double fc = cc == 0 ? f0 : (cc == 1 ? f1 : f2);
-            rhs = fma(pc[nc][cc], wz * fc - jn0, rhs);
-            for (int w = 0; w < NW; ++w) row[w] = fma(pc[nc][cc], sJW[(3 * k + cc) * NW + w], row[w]);
+            rhs = fma(pn[cc], wz * fc - jn0, rhs);
+            for (int w = 0; w < NW; ++w) row[w] = fma(pn[cc], sJW[(3 * k + cc) * NW + w], row[w]);
           }
           sb[n++] = -rhs;   // row . nu_w = -rhs
           ++nc;
@@ -225,14 +250,7 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
         v = 0.0;
         for (int t = j; t < n; ++t) v = fma(A[t * NW + lane], A[t * NW + lane], v);
       }
-      for (int o = kWave / 2; o > 0; o >>= 1) {   // the largest, the lowest column among ties
-        const double ov = __shfl_xor(v, o, kWave);
-        const int op = __shfl_xor(p, o, kWave);
-        if (ov > v || (ov == v && op < p)) {
-          v = ov;
-          p = op;
-        }
-      }
+      wave_argmax_fast(v, p);   // the largest, the lowest column among ties (same butterfly order)
       const double cn = sqrt(v);
       if (j == 0) nmax0 = cn;
       if (!(cn > 1e-10 * nmax0) || cn == 0.0) break;

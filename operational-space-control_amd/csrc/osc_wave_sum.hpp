@@ -89,4 +89,24 @@ __device__ __forceinline__ void wave_argmin_fast(double& v, int& idx) {
   argmin_level<1>(v, idx, lane);
 }
 
+// (value, index) maximum with the lowest index among ties (the dual kernel's column pivoting)
+template <int O>
+__device__ __forceinline__ void argmax_level(double& v, int& idx, int lane) {
+  const double ov = xor_partner<O>(v, lane);
+  const int oi = static_cast<int>(xor_partner_u32<O>(static_cast<unsigned>(idx), lane));
+  if (ov > v || (ov == v && oi < idx)) {
+    v = ov;
+    idx = oi;
+  }
+}
+__device__ __forceinline__ void wave_argmax_fast(double& v, int& idx) {
+  const int lane = wave_lane();
+  argmax_level<32>(v, idx, lane);
+  argmax_level<16>(v, idx, lane);
+  argmax_level<8>(v, idx, lane);
+  argmax_level<4>(v, idx, lane);
+  argmax_level<2>(v, idx, lane);
+  argmax_level<1>(v, idx, lane);
+}
+
 }  // namespace osc

@@ -8,7 +8,7 @@ O=gpurun_out/${DU_OUT:-r05du2}
 mkdir -p $O
 OSC_LIB_PATH=operational-space-control_amd/lib/duprof/libosc_batch.so timeout -k 10 300 python tools/wheel_census.py 2048 91 tumbling bernoulli 1 '{}' --brief > $O/dual_profile.txt 2> $O/err.txt || exit 30
 for seed in 91 92; do
-for lib in ab_old/libosc_batch.so libosc_batch.so; do
+for lib in ${AB_BASE:-ab_old}/libosc_batch.so libosc_batch.so; do
   for sc in "tumbling bernoulli" "standing ones"; do
     OSC_LIB_PATH=operational-space-control_amd/lib/$lib timeout -k 10 300 python tools/wheel_census.py 2048 $seed $sc 1 '{}' --brief >> $O/wheel_ab.jsonl 2>> $O/wheel_ab.err || exit 31
   done

@@ -84,7 +84,8 @@ def main():
                "iters_mean": float(out.iters.float().mean().item()),
                "iters_max": int(out.iters.max().item()), "ms": ms,
                "tau_x_sha": hashlib.sha1(out.tau.cpu().numpy().tobytes() +
-                                         out.x.cpu().numpy().tobytes()).hexdigest()[:16]}
+                                         out.x.cpu().numpy().tobytes()).hexdigest()[:16],
+               "y_sha": hashlib.sha1(out.y.cpu().numpy().tobytes()).hexdigest()[:16]}
         print(json.dumps(row), flush=True)
         tau = out.tau.cpu().numpy()
         it = out.iters.cpu().numpy()
