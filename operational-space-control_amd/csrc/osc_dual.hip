@@ -23,7 +23,10 @@ namespace osc {
 // the wrong sign or one on an inactive bound -- the KKT certificate of tests/test_gpu_wheels.py.
 // One 64-lane wavefront per env; M is factored in LDS (left-looking Cholesky, lane = row).
 template <class D>
-__global__ __launch_bounds__(kWave) void osc_dual_kernel(
+// (two waves per SIMD at least: with the serial solves' loops rolled the wheel model's kernel
+// needs 124 VGPRs, four waves per SIMD -- it ran one per SIMD at 256 + 28 fully unrolled,
+// 2,048 envs in two rounds of waves: 206 -> 155 us, bitwise, profiles/r05/dual/r05du4_*)
+__global__ __launch_bounds__(kWave, 2) void osc_dual_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gJ, const double* __restrict__ gmask,
     const double* __restrict__ gwd, const double* __restrict__ ws, const double* __restrict__ gx,
@@ -73,11 +76,13 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   DU_T(0);
   // L L' v = b in place (one lane, serial)
   auto chol_solve = [&](double* v) {
+    #pragma unroll 1
     for (int i = 0; i < NV; ++i) {
       double a = v[i];
       for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], v[p], a);
       v[i] = a / sL[i * NV + i];
     }
+    #pragma unroll 1
     for (int i = NV - 1; i >= 0; --i) {
       double a = v[i];
       for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], v[p], a);
@@ -320,11 +325,13 @@ __global__ __launch_bounds__(kWave) void osc_dual_kernel(
   }
   __syncthreads();
   if (lane == 0) {   // L L' nu = -g_x
+    #pragma unroll 1
     for (int i = 0; i < NV; ++i) {
       double a = sg[i];
       for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], sg[p], a);
       sg[i] = a / sL[i * NV + i];
     }
+    #pragma unroll 1
     for (int i = NV - 1; i >= 0; --i) {
       double a = sg[i];
       for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], sg[p], a);
