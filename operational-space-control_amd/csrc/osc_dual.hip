@@ -25,7 +25,8 @@ namespace osc {
 template <class D>
 // (two waves per SIMD at least: with the serial solves' loops rolled the wheel model's kernel
 // needs 124 VGPRs, four waves per SIMD -- it ran one per SIMD at 256 + 28 fully unrolled,
-// 2,048 envs in two rounds of waves: 206 -> 155 us, bitwise, profiles/r05/dual/r05du4_*)
+// 2,048 envs in two rounds of waves: 206 -> 155 us, the inner loops unrolled by four 149 us,
+// bitwise, profiles/r05/dual/r05du{4,5}_*)
 __global__ __launch_bounds__(kWave, 2) void osc_dual_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gJ, const double* __restrict__ gmask,
@@ -79,12 +80,14 @@ __global__ __launch_bounds__(kWave, 2) void osc_dual_kernel(
     #pragma unroll 1
     for (int i = 0; i < NV; ++i) {
       double a = v[i];
+      #pragma unroll 4
       for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], v[p], a);
       v[i] = a / sL[i * NV + i];
     }
     #pragma unroll 1
     for (int i = NV - 1; i >= 0; --i) {
       double a = v[i];
+      #pragma unroll 4
       for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], v[p], a);
       v[i] = a / sL[i * NV + i];
     }
@@ -328,12 +331,14 @@ __global__ __launch_bounds__(kWave, 2) void osc_dual_kernel(
     #pragma unroll 1
     for (int i = 0; i < NV; ++i) {
       double a = sg[i];
+      #pragma unroll 4
       for (int p = 0; p < i; ++p) a = fma(-sL[i * NV + p], sg[p], a);
       sg[i] = a / sL[i * NV + i];
     }
     #pragma unroll 1
     for (int i = NV - 1; i >= 0; --i) {
       double a = sg[i];
+      #pragma unroll 4
       for (int p = i + 1; p < NV; ++p) a = fma(-sL[p * NV + i], sg[p], a);
       sg[i] = a / sL[i * NV + i];
     }
