@@ -3,7 +3,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 export TMPDIR=/tmp
-O=gpurun_out/r05wt
+O=gpurun_out/${WT_OUT:-r05wt}
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run --output-format csv -- python3 tools/wheel_census.py 2048 91 tumbling bernoulli 1 '{}' --brief > $O/census.jsonl 2> $O/err.txt || exit 31
 echo done
