@@ -252,6 +252,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
     if (lane < NX) {
       double z1 = 0.0;
       int j = q;
+#pragma unroll 4
       for (; j + 1 < NX; j += 2) {
         zi = fma(sJ[lane * NXP + j], sd[j], zi);
         z1 = fma(sJ[lane * NXP + j + 1], sd[j + 1], z1);

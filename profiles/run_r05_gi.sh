@@ -6,7 +6,7 @@ cd "$R"
 O=gpurun_out/${GI_OUT:-r05gi}
 mkdir -p $O
 for seed in 91 92; do
-for lib in ab_old/libosc_batch.so libosc_batch.so; do
+for lib in ${AB_BASE:-ab_old}/libosc_batch.so libosc_batch.so; do
   for sc in "tumbling bernoulli" "standing ones"; do
     OSC_LIB_PATH=operational-space-control_amd/lib/$lib timeout -k 10 300 python tools/wheel_census.py 2048 $seed $sc 1 '{}' --brief >> $O/wheel_ab.jsonl 2>> $O/wheel_ab.err || exit 31
   done
