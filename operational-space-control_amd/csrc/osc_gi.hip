@@ -410,25 +410,12 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
   if (lane < NX) sx[lane] = xi;
   __syncthreads();
   // ---- one-sided rows ----
+  // the working one-sided rows as a bit set over p, wave-uniform, kept as rows join and leave
+  // (was: rebuilt from the lanes' ids by a 64-lane OR butterfly every step; the same set)
+  unsigned long long in_set = 0ull;
   while (ok) {
     if (++steps > kMaxSteps) { ok = false; break; }
     GI_T0();
-    // working one-sided rows as a bit set over p
-    unsigned long long in_set = (lane < q && act >= kIneq) ? (1ull << (act - kIneq)) : 0ull;
-    {
-      auto orx = [&](auto O) {
-        constexpr int o = decltype(O)::value;
-        const unsigned lo = xor_partner_u32<o>(static_cast<unsigned>(in_set), lane);
-        const unsigned hi = xor_partner_u32<o>(static_cast<unsigned>(in_set >> 32), lane);
-        in_set |= (static_cast<unsigned long long>(hi) << 32) | lo;
-      };
-      orx(std::integral_constant<int, 32>{});
-      orx(std::integral_constant<int, 16>{});
-      orx(std::integral_constant<int, 8>{});
-      orx(std::integral_constant<int, 4>{});
-      orx(std::integral_constant<int, 2>{});
-      orx(std::integral_constant<int, 1>{});
-    }
     const double xs = wmax(lane < NX ? fabs(xi) : 0.0);
     double viol = INFINITY;
     int p = lane;
@@ -467,6 +454,7 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       __syncthreads();
       if (t2 <= t1) {   // full step: p joins
         if (lane == q) act = kIneq + p;
+        in_set |= 1ull << p;
         GI_T0();
         add_row();
         GI_T1(4);
@@ -475,6 +463,10 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
 #endif
         ++q;
         break;
+      }
+      {   // (kd: a one-sided row -- t1 only comes from those)
+        const int kdu = __builtin_amdgcn_readfirstlane(kd);
+        in_set &= ~(1ull << (__builtin_amdgcn_readlane(act, kdu) - kIneq));
       }
       GI_T0();
       drop_row(kd);
