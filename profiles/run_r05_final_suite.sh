@@ -2,7 +2,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
-O=gpurun_out/r05fin
+O=gpurun_out/${FIN_OUT:-r05fin}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 31
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 32
