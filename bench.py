@@ -402,6 +402,100 @@ def warm_ticks(solver, inputs, nenv: int, steps: int, warmup: int, seed: int, st
                         "ping-pong, warm state carried between ticks"}
 
 
+def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=None) -> dict | None:
+    """SURVEY.md §8(e)'s data path: every tick's inputs start in PINNED HOST
+    memory -- where the reference's control loop finds them (operational_space_controller.h:
+    546-573) -- cross PCIe in one H2D copy, are solved, and tau / status / iters come back
+    (include/osc_host_feed.h).  Depth 2: tick k's copy overlaps tick k-1's solve.  Two input forms:
+    post-kinematics QP inputs (M, C, J, b, T, mask: 7,664 B per Go2 env) and joint states (qpos,
+    qvel, T, mask through the GPU kinematics: 568 B).  Each rank runs its own feed (its own pinned
+    buffers, its own host thread = the rank process); value = all ranks' envs x ticks / the slowest
+    rank's time.  The producer's writes are not timed (the inputs of two ticks are written once
+    into the two pinned slots, alternating); each tick still waits for its slot as a producer
+    would.  Stage durations by HIP events on each stage's stream (the last ticks).  Reported
+    beside the headline (whose inputs are HBM-resident), never as it."""
+    if feed_cls is None:
+        from osc_amd.host_feed import HostFeed as feed_cls
+    if kin_cls is None:
+        from osc_amd.kinematics import KinematicsBatch as kin_cls
+    from osc_amd.kinematics import load_tree, random_states
+    robot = solver.robot
+    sizes = [int(s) for s in args.host_fed_envs.split(",") if s.strip()]
+    res = {"robot": robot, "depth": args.host_fed_depth, "per_gpu": {}}
+    tree = load_tree(robot)
+    kin = kin_cls(tree=tree)
+    steps, warmup = max(args.steps, 10), max(args.warmup, 4)
+    for nenv in sizes:
+        d = [generate(robot, nenv, shard_seed(rank) + 40 + k, args.scenario, args.mask)
+             for k in range(2)]
+        qs = [random_states(tree, nenv, shard_seed(rank) + 50 + k, joint_range=0.5)
+              for k in range(2)]
+        for form in ("qp", "joint_states"):
+            row = {}
+            for depth in (args.host_fed_depth, 1):
+                feed = feed_cls(solver, nenv, form, depth=depth,
+                                kin=kin if form == "joint_states" else None)
+                tick = [0]
+
+                def step(fill=False):
+                    k = tick[0]
+                    v = feed.inputs(k)
+                    if fill:
+                        src = d[k % 2]
+                        if form == "qp":
+                            for key in ("M", "C", "J", "b"):
+                                v[key][...] = src[key]
+                        else:
+                            v["qpos"][...], v["qvel"][...] = qs[k % 2]
+                        v["T"][...], v["mask"][...] = src["T"], src["mask"]
+                    feed.submit(k)
+                    if k >= depth - 1:
+                        feed.wait(k - depth + 1)
+                    tick[0] += 1
+
+                for w in range(warmup):
+                    step(fill=w < 2)
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    step()
+                for j in range(tick[0] - depth + 1, tick[0]):   # drain the pipeline
+                    feed.wait(j)
+                elapsed = time.perf_counter() - t0
+                barrier()
+                last = tick[0] - 1
+                tau, status, _ = feed.wait(last)
+                conv = int((np.asarray(status) == 0).sum())
+                tims = [feed.timing(j) for j in range(max(0, last - depth + 1), last + 1)]
+                stats = reduce_stats(world, dev, nenv, elapsed, 0.0, 0.0, conv)
+                h2d = float(np.mean([t["h2d_ms"] for t in tims]))
+                sol = float(np.mean([t["solve_ms"] for t in tims]))
+                d2h = float(np.mean([t["d2h_ms"] for t in tims]))
+                period = stats.elapsed_s / steps * 1e3
+                serial = h2d + sol + d2h
+                longest = max(h2d, sol, d2h)
+                entry = {"value": job_value(stats, steps), "unit": "solves/s",
+                         "ms_per_tick": period, "h2d_ms": h2d, "solve_ms": sol, "d2h_ms": d2h,
+                         "h2d_bytes": int(feed.in_bytes), "d2h_bytes": int(feed.out_bytes),
+                         "h2d_GBps": feed.in_bytes / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
+                         "bytes_per_env_h2d": feed.in_bytes / nenv,
+                         "converged_frac": stats.converged,
+                         "global_envs": stats.total_envs}
+                if depth > 1:
+                    entry["overlap_frac"] = ((serial - period) / (serial - longest)
+                                             if serial > longest else None)
+                    entry["bound"] = "h2d (PCIe)" if h2d >= sol else "solve"
+                    row.update(entry)
+                else:
+                    row["serial_depth1"] = {k: entry[k] for k in ("value", "ms_per_tick")}
+                feed.close()
+            res["per_gpu"].setdefault(str(nenv), {})[form] = row
+    res["note"] = ("overlap_frac = (h2d + solve + d2h - period) / (h2d + solve + d2h - longest "
+                   "stage): 1 = every stage but the longest hidden; serial_depth1 = the same "
+                   "ticks with one slot (copies and solve in series)")
+    return res if rank == 0 else None
+
+
 def baseline_config_tag(args, nenv):
     """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
     tags = {("unitree_go2", "standing", "ones", 4096): 1,
@@ -478,6 +572,12 @@ def parse_args(argv=None):
     ap.add_argument("--hbm-batches", type=int, default=10,
                     help="roofline.hbm_inputs: rotate this many copies of the batch (> 256 MB of "
                          "inputs: past the Infinity Cache); 0 = off")
+    ap.add_argument("--host-fed-envs", default="4096,8192",
+                    help="per-GPU batches of the host_fed object (SURVEY.md §8(e): inputs from "
+                         "pinned host memory every tick); empty = off")
+    ap.add_argument("--host-fed-depth", type=int, default=2,
+                    help="pipeline slots of the host-fed tick (2 = H2D of tick k overlaps the "
+                         "solve of tick k-1)")
     ap.add_argument("--hbm-only", action="store_true",
                     help="run only the HBM-input rotation (for rocprofv3 --pmc passes)")
     ap.add_argument("--hbm-traffic-json",
@@ -747,7 +847,7 @@ def single_env(robot: str, ticks: int) -> dict:
 
 def ipm_kernel_name(robot: str, nenv: int, dev) -> str:
     """The interior-point kernel(s) one launch runs: past one resident wavefront per SIMD the
-    cold WaLTER solve of at least four rounds of wavefronts runs the lockstep compaction's park and resume passes (csrc/osc_batch.hip,
+    cold WaLTER solve of at least four rounds of wavefronts runs the lockstep compaction's park and resume passes (csrc/osc_ipm.hpp,
     ParkArgs; the default park iteration, osc_model_tuning.park_it, is 16 for WaLTER, off for Go2)."""
     cus = (torch.cuda.get_device_properties(dev).multi_processor_count
            if torch.cuda.is_available() else 256)   # (CPU rehearsal of the rank path: MI355X)
@@ -803,8 +903,14 @@ def main(argv=None) -> None:
     objs = multi_gpu_objects(args, world, rank, dev, barrier, OSCBatchSolver, clock)
     line, solver, inputs = run_headline(args, world, rank, dev, barrier, OSCBatchSolver, clock,
                                         prepared)
+    # SURVEY.md §8(e)'s host-fed tick: every rank its own pinned feed (after the headline's timed
+    # region, so its PCIe traffic never overlaps it)
+    hf = (host_fed(args, world, rank, dev, barrier, solver)
+          if args.host_fed_envs.strip() and args.robot != "mixed" else None)
     if line is not None:
         line.update(objs)
+        if hf is not None:
+            line["host_fed"] = hf
         line["clocks"] = ("the headline's timed steps run after the north_star / mixed lines "
                           "(GPU clocks at a running loop's level, not an idle GPU's ramp)")
     if line is not None:

@@ -267,7 +267,9 @@ typedef struct {
   void* workspace;
   size_t workspace_bytes;
   const double* wheel_dir;        /* (ABI 4) [nenv][nc][6] DEVICE; required iff the model has wheel
-                                     rows (osc_solve_extras.wheel_dir), else ignored            */
+                                     rows (osc_solve_extras.wheel_dir); MUST be NULL otherwise
+                                     (a non-NULL one is refused: OSC_ERR_INVALID_ARGUMENT, the
+                                     mark of a job built against the ABI-3 layout)              */
 } osc_batch_job;
 
 /* Several robots' batches on one GPU in one call (BASELINE configs[4]: Go2 + WaLTER Sr shards

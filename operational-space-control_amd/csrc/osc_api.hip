@@ -451,10 +451,19 @@ extern "C" int osc_batch_solve_multi(const osc_batch_job* jobs, int32_t njobs, v
     if (j.model->kid == K_NONE) return OSC_ERR_UNSUPPORTED_DIMS;
     if (j.model->kid == K_WALTER_WHEELS && (!j.wheel_dir || misaligned16(j.wheel_dir)))
       return OSC_ERR_INVALID_ARGUMENT;
+    // wheel_dir must be NULL without wheel rows: a non-NULL one there is the mark of a caller
+    // built against the ABI-3 job layout
+    if (j.model->kid != K_WALTER_WHEELS && j.wheel_dir != nullptr) return OSC_ERR_INVALID_ARGUMENT;
     if (!on_model_device(j.model)) return OSC_ERR_INVALID_ARGUMENT;   // one device per call
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (njobs == 2 && jobs[0].nenv > 0 && jobs[1].nenv > 0 && jobs[0].model->kid != jobs[1].model->kid &&
+  // The two-model grid exists for exactly {walter_sr, unitree_go2} (a wheel-row model
+  // next to either must not take it -- its kernels, strides and fallback differ).
+  const auto kid_pair = [&](KernelId p, KernelId q) {
+    return jobs[0].model->kid == p && jobs[1].model->kid == q;
+  };
+  if (njobs == 2 && jobs[0].nenv > 0 && jobs[1].nenv > 0 &&
+      (kid_pair(K_WALTER, K_GO2) || kid_pair(K_GO2, K_WALTER)) &&
       jobs[0].nenv <= jobs[0].model->small_batch_max && jobs[1].nenv <= jobs[1].model->small_batch_max) {
     const bool a_walter = jobs[0].model->kid == K_WALTER;
     const osc_batch_job& w = a_walter ? jobs[0] : jobs[1];   // slower per wavefront: first

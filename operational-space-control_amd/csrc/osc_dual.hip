@@ -12,7 +12,9 @@ namespace osc {
 // sign convention (H x + f + A'y = 0, y >= 0 on an active upper bound, <= 0 on a lower one),
 // recovered from the returned design vector x = (dv, u, z) by stationarity:
 //   dynamics rows  nu = -M^-1 (H_dv dv + f_dv + E'nu_w)             (the dv block)
-//   wheel rows     nu_w = R'(w - V g0) from the refinement's multipliers w (W_NU)
+//   wheel rows     nu_w by least squares on stationarity itself (below; the interior point's W_NU
+//                  is not read: it exists only where the refinement was kept, and the active-set
+//                  fallback's envs have none -- ADVICE r5)
 //   u box rows     nu_a - 2 (w_tau + w_reg) u                        (the u block)
 //   contact k      r_k = 2 w_reg z_k - Jc_k'nu must be balanced by its active rows: the pyramid
 //                  rows, fz >= 0, fz <= big_number (a tiny non-negative least squares over the

@@ -496,7 +496,9 @@ __global__ __launch_bounds__(kWave) void osc_gi_kernel(
       s = fma(sE[lane * NXP + i], sx[i], s);
       cm = fmax(cm, fabs(sE[lane * NXP + i]));
     }
-    bad = fabs(s) / (1.0 + cm * xs + fabs(sEb[lane])) <= 1e-8 ? 0.0 : 1.0;   // (NaN: bad)
+    // combined with the sign test above, never assigned over it: working one-sided rows sit at
+    // lanes below neq whenever a dependent equality row was skipped
+    if (!(fabs(s) / (1.0 + cm * xs + fabs(sEb[lane])) <= 1e-8)) bad = 1.0;   // (NaN: bad)
   }
   if (lane < NX && !isfinite(xi)) bad = 1.0;
   if (in_valid(lane) &&

@@ -730,9 +730,9 @@ __device__ __forceinline__ void ipm_block(
   };
   bool parked = false;   // park pass: this row's env went to the park area (no outputs here)
   bool refined = false;
-  // WH with the duals requested: the wheel rows' multipliers for the dual kernel (W_NU; the
-  // refinement's where it is kept, else the interior point's centre).  The dual kernel recovers
-  // every other multiplier from the design vector itself.
+  // WH with the duals requested: the wheel rows' multipliers (W_NU; the refinement's where it is
+  // kept, else the interior point's centre) -- a diagnostic of the workspace since round 4: the
+  // dual kernel recovers every multiplier, the wheel rows' included, from the design vector.
   // (w = L' nu: the multipliers of the rows [V X | V x0 - vs] before their orthonormalisation,
   // which the dual kernel maps back to E's rows; every lane of the env's row takes part)
   auto put_wheel_duals = [&](double nu) {

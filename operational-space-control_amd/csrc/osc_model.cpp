@@ -214,7 +214,7 @@ extern "C" int osc_desc_from_yaml(const char* robot, const char* yaml_path, osc_
   desc->z_lb[0] = -inf; desc->z_lb[1] = -inf; desc->z_lb[2] = 0.0;
   desc->z_ub[0] = inf;  desc->z_ub[1] = inf;  desc->z_ub[2] = big_number;
   desc->infinity = inf;
-  // interior-point stop.  The full-space refinement that follows (osc_batch.hip) needs only an
+  // interior-point stop.  The full-space refinement that follows (osc_ipm.hpp) needs only an
   // approximate active set: its rounds add the rows its point violates and drop the rows whose
   // multiplier comes out negative, and it is kept only at a KKT point.  So the
   // interior point stops early -- Go2 at 1e-6, WaLTER at 1e-8 (numpy model of the kernel,

@@ -35,7 +35,9 @@ EXPORTED_SYMBOLS = ("osc_desc_from_yaml", "osc_model_create", "osc_model_create_
                     "osc_contact_geom_table", "osc_tumbling_params_default",
                     "osc_tumbling_targets", "osc_dual_rows", "osc_batch_solve_ex",
                     "osc_batch_assemble_ex", "osc_model_tuning_defaults",
-                    "osc_model_create_tuned", "osc_batch_solve_warm_ex")
+                    "osc_model_create_tuned", "osc_batch_solve_warm_ex",
+                    "osc_host_feed_create", "osc_host_feed_destroy", "osc_host_feed_inputs",
+                    "osc_host_feed_submit", "osc_host_feed_wait", "osc_host_feed_timing")
 
 OSC_KIN_MAX_BODIES = 16
 OSC_KIN_MAX_DOFS = 32
@@ -111,6 +113,27 @@ class OscKinDesc(ctypes.Structure):
         ("site_body", ctypes.c_int32 * _S), ("site_pos", (ctypes.c_double * 3) * _S),
         ("has_jac_body", ctypes.c_int32), ("site_jac_body", ctypes.c_int32 * _S),
     ]
+
+
+class OscFeedInputs(ctypes.Structure):
+    """osc_feed_inputs (include/osc_host_feed.h): pinned host pointers of one slot's inputs."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("M", "C", "J", "b", "qpos", "qvel", "T",
+                                                "contact_mask")] + [("bytes", ctypes.c_size_t)]
+
+
+class OscFeedOutputs(ctypes.Structure):
+    """osc_feed_outputs (include/osc_host_feed.h): pinned host pointers of one tick's outputs."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("tau", "status", "iters")] + \
+        [("bytes", ctypes.c_size_t)]
+
+
+class OscFeedTiming(ctypes.Structure):
+    """osc_feed_timing (include/osc_host_feed.h): per-stage HIP-event durations (ms)."""
+    _fields_ = [(n, ctypes.c_float) for n in ("h2d_ms", "solve_ms", "d2h_ms",
+                                               "h2d_start_to_d2h_end_ms")]
+
+
+FEED_QP, FEED_JOINT_STATES, FEED_WARM = 0, 1, 1
 
 
 class OSCError(RuntimeError):
@@ -222,6 +245,18 @@ def lib() -> ctypes.CDLL:
     L.osc_batch_solve_qpos_warm.argtypes = [vp, vp, i32] + [vp] * 9 + [ctypes.c_size_t, vp,
                                                                       ctypes.c_size_t, vp]
     L.osc_batch_solve_qpos_warm.restype = ctypes.c_int
+    L.osc_host_feed_create.argtypes = [vp, vp, i32, i32, ctypes.c_uint32, i32, ctypes.POINTER(vp)]
+    L.osc_host_feed_create.restype = ctypes.c_int
+    L.osc_host_feed_destroy.argtypes = [vp]
+    L.osc_host_feed_destroy.restype = ctypes.c_int
+    L.osc_host_feed_inputs.argtypes = [vp, i32, ctypes.POINTER(OscFeedInputs)]
+    L.osc_host_feed_inputs.restype = ctypes.c_int
+    L.osc_host_feed_submit.argtypes = [vp, i32]
+    L.osc_host_feed_submit.restype = ctypes.c_int
+    L.osc_host_feed_wait.argtypes = [vp, i32, ctypes.POINTER(OscFeedOutputs)]
+    L.osc_host_feed_wait.restype = ctypes.c_int
+    L.osc_host_feed_timing.argtypes = [vp, i32, ctypes.POINTER(OscFeedTiming)]
+    L.osc_host_feed_timing.restype = ctypes.c_int
     _lib = L
     return L
 

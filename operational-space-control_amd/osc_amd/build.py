@@ -28,7 +28,7 @@ ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 # kernel units (csrc/osc_device.hpp lists what each holds) + host units
 SOURCES = ["osc_ipm_go2.hip", "osc_ipm_walter.hip", "osc_ipm_wheels.hip", "osc_multi.hip",
            "osc_setup.hip", "osc_gi.hip", "osc_dual.hip", "osc_kinematics.hip",
-           "osc_producers.hip", "osc_api.hip", "osc_model.cpp", "osc_mjcf.cpp"]
+           "osc_producers.hip", "osc_api.hip", "osc_model.cpp", "osc_mjcf.cpp", "osc_host_feed.cpp"]
 HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp", "osc_kin_device.hpp",
            "osc_qpos.hpp", "osc_wave_sum.hpp"]
 # device-code units, for the static checks that read the generated assembly
@@ -54,7 +54,7 @@ def build(verbose: bool = False, force: bool = False, out: str | None = None,
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + \
         [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h",
-                                                     "osc_kinematics.h")] + [__file__]
+                                                     "osc_kinematics.h", "osc_host_feed.h")] + [__file__]
     variant = out != OUT
     if not force and os.path.exists(out):
         t_out = os.path.getmtime(out)

@@ -12,7 +12,8 @@ from osc_amd import _lib
 from osc_qp import load_model
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h", "osc_kinematics.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("osc_batch.h", "osc_producers.h", "osc_kinematics.h",
+                                                               "osc_host_feed.h")]
 REF_CONFIG = "/root/reference/config"
 
 
@@ -96,7 +97,7 @@ def test_reads_reference_yaml_files(robot, rel):
     np.testing.assert_array_equal(np.array(d.w_pos[:m.ns]), m.w_pos)
     np.testing.assert_array_equal(np.array(d.w_rot[:m.ns]), m.w_rot)
     assert d.mu == m.mu
-    # a model the library has a kernel for (select_kernel, csrc/osc_batch.hip)
+    # a model the library has a kernel for (select_kernel, csrc/osc_device.hpp)
     h = ctypes.c_void_p()
     rc = _lib.lib().osc_model_create(ctypes.byref(d), ctypes.byref(h))
     assert rc != 2, rel            # not OSC_ERR_UNSUPPORTED_DIMS (CPU-only: OSC_ERR_NO_DEVICE)

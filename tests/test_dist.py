@@ -81,6 +81,53 @@ class _StubSolver:
         out.status.zero_()
 
 
+class _StubFeed:
+    """Host stand-in for osc_amd.host_feed.HostFeed (pinned slots -> H2D -> solve -> D2H): the
+    slot / tick bookkeeping of include/osc_host_feed.h on numpy buffers, no device."""
+
+    def __init__(self, solver, nenv, form="qp", depth=2, warm=False, kin=None):
+        from osc_amd.robots import dims
+        d = dims(solver.robot)
+        self.nenv, self.form, self.depth, self.next = nenv, form, depth, 0
+        shapes = {"T": (nenv, d["ns"], 6), "mask": (nenv, d["nc"])}
+        if form == "qp":
+            shapes.update(M=(nenv, d["nv"], d["nv"]), C=(nenv, d["nv"]),
+                          J=(nenv, d["s"], d["nv"]), b=(nenv, d["s"]))
+        else:
+            assert kin is not None
+            shapes.update(qpos=(nenv, d["nv"] + 1), qvel=(nenv, d["nv"]))
+        self.slots = [{k: np.zeros(v) for k, v in shapes.items()} for _ in range(depth)]
+        self.in_bytes = sum(a.nbytes for a in self.slots[0].values())
+        self.out_bytes = nenv * (d["nu"] * 8 + 8)
+        self.done, self.nu = {}, d["nu"]
+
+    def inputs(self, k):
+        assert k == self.next
+        return self.slots[k % self.depth]
+
+    def submit(self, k):
+        assert k == self.next
+        src = self.slots[k % self.depth]
+        first = src["M"][:, 0, :self.nu] if self.form == "qp" else src["qpos"][:, :self.nu]
+        self.done[k] = (first.copy(), np.zeros(self.nenv, np.int32), np.full(self.nenv, 10, np.int32))
+        self.next += 1
+
+    def wait(self, k):
+        assert self.next - self.depth <= k < self.next
+        return self.done[k]
+
+    def timing(self, k):
+        return {"h2d_ms": 0.3, "solve_ms": 0.2, "d2h_ms": 0.01, "latency_ms": 0.6}
+
+    def close(self):
+        pass
+
+
+class _StubKin:
+    def __init__(self, tree=None):
+        self.tree = tree
+
+
 def _stub_multi(jobs, stream=None):
     for solver, out, inputs in jobs:
         solver.solve_into(out, *inputs)
@@ -102,6 +149,14 @@ def _bench_worker(rank, world, port, out_dir):
         bench.attach_multi_gpu_objects(args, world, rank, dev, lambda: barrier(world), _StubSolver,
                                        clock, line, multi_fn=_stub_multi)
         np.save(os.path.join(out_dir, f"M{rank}.npy"), inputs[0].numpy())
+        # every rank its own host feed (pinned slots, its own host thread)
+        args.host_fed_envs = "16,32"
+        hf = bench.host_fed(args, world, rank, dev, lambda: barrier(world), _StubSolver("unitree_go2"),
+                            feed_cls=_StubFeed, kin_cls=_StubKin)
+        if line is not None:
+            line["host_fed"] = hf
+        else:
+            assert hf is None
         if rank == 0:
             with open(os.path.join(out_dir, "line.json"), "w") as fh:
                 json.dump(line, fh)
@@ -133,6 +188,16 @@ def test_bench_rank_path_two_gloo_ranks(tmp_path):
     mx = line["mixed"]
     assert mx["config"]["global_envs"] == 2 * 2 * 8 and mx["config"]["envs_per_gpu"] == 16
     assert mx["converged_frac"] == 1.0
+    # host-fed tick: per-GPU batches 16 and 32, both input forms, every rank's envs counted
+    hf = line["host_fed"]
+    assert hf["depth"] == 2 and set(hf["per_gpu"]) == {"16", "32"}
+    for nenv in (16, 32):
+        for form in ("qp", "joint_states"):
+            r = hf["per_gpu"][str(nenv)][form]
+            assert r["global_envs"] == 2 * nenv and r["converged_frac"] == 1.0
+            assert r["h2d_GBps"] > 0 and r["bound"] == "h2d (PCIe)"
+            assert r["value"] > 0 and r["serial_depth1"]["value"] > 0
+            assert r["bytes_per_env_h2d"] == (7664 - 96 if form == "qp" else (19 + 18 + 30 + 4) * 8)
 
 
 def test_bench_launcher(monkeypatch):

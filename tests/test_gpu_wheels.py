@@ -502,3 +502,35 @@ def test_wheel_model_in_solve_multi(gpu):
     for (s, o, *_), r in zip(jobs, solo):
         for k in ("tau", "x", "status", "iters"):
             assert torch.equal(getattr(o, k), getattr(r, k)), (s.robot, k)
+
+
+@pytest.mark.parametrize("order", [("noslip", "unitree_go2"), ("unitree_go2", "noslip"),
+                                   ("noslip", "walter_sr"), ("walter_sr", "noslip")])
+def test_wheel_model_in_two_job_multi(gpu, order):
+    """Two jobs, one of them a wheel-row model: the two-model grid is only for
+    {walter_sr, unitree_go2}, so either order runs each job as its own call -- bitwise."""
+    from osc_amd.solver import solve_multi_into
+    wheel = _wheel()
+    robots = {"unitree_go2": "unitree_go2", "noslip": "walter_sr_wheels", "walter_sr": "walter_sr"}
+    jobs, solo = [], []
+    for i, key in enumerate(order):
+        s = solver(key)
+        robot = robots[key]
+        d = generate(robot, 192 + 64 * i, SEED_BASE + 211 + i, "tumbling", "bernoulli")
+        args = s.prepare(**d)
+        wdt = None
+        if key == "noslip":
+            wdt = torch.from_numpy(wheel_directions(robot, d, wheel.dof, wheel.radius,
+                                                    SEED_BASE + 221 + i)).cuda()
+        n = d["M"].shape[0]
+        o = s.alloc_outputs(n, want_x=True)
+        jobs.append((s, o, args) + ((wdt,) if wdt is not None else ()))
+        r = s.alloc_outputs(n, want_x=True)
+        s.solve_into(r, *args, wheel_dir=wdt)
+        solo.append(r)
+    solve_multi_into(jobs)
+    torch.cuda.synchronize()
+    for (s, o, *_), r in zip(jobs, solo):
+        assert (r.status.cpu().numpy() == 0).all(), s.robot
+        for k in ("tau", "x", "status", "iters"):
+            assert torch.equal(getattr(o, k), getattr(r, k)), (s.robot, k)
