@@ -205,6 +205,20 @@ template <class D, bool SMALL, int RF>
 constexpr bool ipm_hrl() {   // Hr kept in LDS across the interior point's iterations
   return SMALL && RF != kRfOnly && hr_fits_lds<D>();
 }
+// Two-wave variant (round 6): Hr's first column slot -- columns 0..15, every row
+// (NY x 16 doubles per env) -- is staged into LDS once per solve, and only the second slot's
+// columns are read from the workspace each iteration, as ROWS 16..NY-1 of Hr (Hr is stored exactly
+// symmetric, so row j = column j bitwise): per-lane contiguous 16-byte loads over a contiguous
+// (NY - 16) x NY block.  At 8,192 Go2 envs every Hr re-read used to miss L2 (37.7 MB of Hr against
+// 8 x 4 MB of L2: 7x the algorithmic bytes); the streamed part is now 1.5 KB per env (12 MB).
+// LDS: 246 + 384 doubles per env, 20.2 KB per wave -- eight waves per CU in 160 KB.
+template <class D, bool SMALL, int RF>
+constexpr bool ipm_hrh() {
+  return !SMALL && !D::WH && RF != kRfOnly && D::NY > kRow &&
+         (IpmLayout<D, false>::IL + D::NY * kRow) * 8 * kEnvPerWave * 8 <= 160 * 1024;
+}
+template <class D, bool SMALL, int RF>
+constexpr int hrh_lds_extra() { return ipm_hrh<D, SMALL, RF>() ? D::NY * kRow : 0; }
 // LDS doubles per env beyond the interior point's layout: the refinement's [X | H_dv | f_dv]
 // block, except that a fused pass with Hr in LDS moves X into Hr's region once the first K_A is
 // assembled (registers hold it from then on) and only keeps [H_dv | f_dv] apart.
@@ -236,7 +250,8 @@ constexpr int refine_lds_extra() {
 // already hidden, and the packed addressing costs issue slots).
 template <class D, bool SMALL, int RF = kRfNone>
 constexpr int ipm_lds_doubles() {
-  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>();
+  constexpr int il = IpmLayout<D, ipm_hrl<D, SMALL, RF>()>::IL + refine_lds_extra<D, SMALL, RF>() +
+                     hrh_lds_extra<D, SMALL, RF>();
   return SMALL ? cmax(kEnvPerWave * il, 160 * 1024 / 5 / 8 + 2) : kEnvPerWave * il;
 }
 
@@ -286,8 +301,10 @@ __device__ __forceinline__ void ipm_block(
     write_out = valid && (!fixup || redo);
   }
 
-  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>();
+  constexpr bool HRH = ipm_hrh<D, SMALL, RF>();
+  constexpr int kEnvLds = LY::IL + refine_lds_extra<D, SMALL, RF>() + hrh_lds_extra<D, SMALL, RF>();
   double* B = sm + grp * kEnvLds;
+  double* sHh = B + LY::IL + refine_lds_extra<D, SMALL, RF>();   // HRH: Hr[i][0..15] at i * 16
   // refinement: [X | H_dv | f_dv] of this env; a fused pass with Hr in LDS keeps X in Hr's region
   constexpr bool kXinHr = RF == kRfFused && HRL;
   double* sRX = kXinHr ? B + LY::I_HR : B + LY::IL + RefineLds<D>::X;
@@ -356,6 +373,19 @@ __device__ __forceinline__ void ipm_block(
     if (l < NC) sMask[l] = mk;
   }
   const double* sHr = B + LY::I_HR;
+  if constexpr (HRH) {   // Hr's first column slot, once per solve
+    static_assert(NY % 2 == 0 && D::WS % 2 == 0 && D::W_HR % 2 == 0, "16-byte Hr row loads");
+#pragma unroll
+    for (int i0 = 0; i0 < NY; i0 += 8) {   // (eight loads in flight: few registers live here)
+      double hv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        hv[i] = i0 + i < NY ? wsw[lane_off + static_cast<unsigned>((i0 + i) * NY + l)] : 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i0 + i < NY) sHh[(i0 + i) * kRow + l] = hv[i];
+    }
+  }
   wave_sync();
 
   // ---- inequality rows of this lane: r = l + 16 t.  Only (active, h) are kept; the row's
@@ -638,6 +668,15 @@ __device__ __forceinline__ void ipm_block(
         c0[i] = hr0[i];
         c1[i] = hr1[i];
       }
+    } else if constexpr (HRH) {
+      unsigned off = lane_off;
+      asm volatile("" : "+v"(off));
+      // column jj1 = row jj1: this lane's contiguous NY doubles, two per 16-byte load
+      const double* p1 = wsw + off + jj1 * NY;
+#pragma unroll
+      for (int i = 0; i < NY; ++i) c1[i] = p1[i];
+#pragma unroll
+      for (int i = 0; i < NY; ++i) c0[i] = sHh[i * kRow + l];
     } else {
       unsigned off = lane_off;
       asm volatile("" : "+v"(off));

@@ -54,12 +54,15 @@ for step in "$@"; do
       timeout -k 10 300 python bench.py --nenv-per-gpu 65536 --steps 50 --warmup 20 $B > "$O/bench_go2_65536.json" 2>> "$O/other.err" &&
       timeout -k 10 300 python bench.py --robot mixed $B > "$O/bench_mixed.json" 2>> "$O/other.err" || exit $((30 + n)) ;;
     pmc)
-      robot=${val%%:*}; nenv=${val#*:}
-      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$R/$O/pmc_fetch_${robot}_${nenv}" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/pmc.err" &&
-      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$R/$O/pmc_write_${robot}_${nenv}" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/pmc.err" || exit $((30 + n)) ;;
+      # -> $O/prof_<robot>_<nenv>/{trace,pmc_fetch,pmc_write}: tools/pmc_summary.py's input layout
+      robot=${val%%:*}; nenv=${val#*:}; P="$R/$O/prof_${robot}_${nenv}"
+      A="--robot $robot --nenv-per-gpu $nenv --steps 10 --warmup 3 $B"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/trace" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" &&
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$P/pmc_fetch" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" &&
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$P/pmc_write" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" || exit $((30 + n)) ;;
     sq)
-      robot=${val%%:*}; nenv=${val#*:}
-      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_ANY -d "$R/$O/sq_${robot}_${nenv}" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/sq.err" || exit $((30 + n)) ;;
+      robot=${val%%:*}; nenv=${val#*:}; P="$R/$O/prof_${robot}_${nenv}"
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_ANY -d "$P/pmc_cyc" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/sq.err" || exit $((30 + n)) ;;
     ab)
       timeout -k 10 500 python tools/ab_time.py "$val" operational-space-control_amd/lib/libosc_batch.so > "$O/ab_$n.jsonl" 2>&1 || exit $((30 + n)) ;;
     hostfed)
