@@ -25,7 +25,7 @@ export TMPDIR=/tmp
 O=gpurun_out/$1
 shift
 mkdir -p "$O"
-B="--no-cpu --no-front-end --no-single-env --no-north-star --no-mixed --hbm-batches 0 --host-fed-envs="
+B="--no-cpu --no-front-end --no-single-env --no-north-star --no-mixed --no-warm --hbm-batches 0 --host-fed-envs="
 n=0
 for step in "$@"; do
   n=$((n + 1))
