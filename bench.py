@@ -496,6 +496,41 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
     return res if rank == 0 else None
 
 
+def staggered(args, solver, inputs, groups: int) -> dict:
+    """The headline's batch as `groups` env groups, each group's ticks in order on its own stream
+    (tick k+1 of a group after its tick k; groups independent) -- how a deployment whose env groups
+    tick out of phase uses the GPU: one group's assembly fills the SIMDs another group's
+    interior-point straggler tail leaves idle (tools/stagger_probe.py).  A step = every env solved
+    once; reported beside the headline, not as it (the headline's step is ONE call over the whole
+    batch: forking and joining streams inside a step measured slower, profiles/r06/
+    stagger_probe.jsonl)."""
+    nenv = inputs[0].shape[0]
+    per = nenv // groups
+    gs = []
+    for g in range(groups):
+        sl = slice(g * per, nenv if g == groups - 1 else (g + 1) * per)
+        inp = tuple(t[sl].contiguous() for t in inputs)
+        gs.append((torch.cuda.Stream(), inp, solver.alloc_outputs(inp[0].shape[0])))
+
+    def step():
+        for st, inp, out in gs:
+            solver.solve_into(out, *inp, stream=st)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    conv = sum(int((out.status == 0).sum().item()) for _, _, out in gs)
+    return {"groups": groups, "envs": nenv, "value": nenv * args.steps / el, "unit": "solves/s",
+            "ms_per_step": el / args.steps * 1e3, "converged_frac": conv / nenv,
+            "workload": f"the headline's {nenv} envs as {groups} groups of {per}, each group's "
+                        f"ticks in order on its own stream, groups out of phase"}
+
+
 def baseline_config_tag(args, nenv):
     """Which BASELINE.json config this workload is (configs[1]..[3] are single-GPU ones)."""
     tags = {("unitree_go2", "standing", "ones", 4096): 1,
@@ -579,6 +614,9 @@ def parse_args(argv=None):
     ap.add_argument("--host-fed-depth", type=int, default=2,
                     help="pipeline slots of the host-fed tick (2 = H2D of tick k overlaps the "
                          "solve of tick k-1)")
+    ap.add_argument("--stagger-groups", type=int, default=4,
+                    help="the `staggered` object beside the headline: its batch as this many env "
+                         "groups ticking out of phase on their own streams; <= 1 = off")
     ap.add_argument("--hbm-only", action="store_true",
                     help="run only the HBM-input rotation (for rocprofv3 --pmc passes)")
     ap.add_argument("--hbm-traffic-json",
@@ -928,6 +966,8 @@ def main(argv=None) -> None:
         if world == 1 and args.hbm_batches > 0:
             line["roofline"]["hbm_inputs"] = hbm_inputs(args, solver, inputs, clock,
                                                          args.hbm_traffic_json)
+        if world == 1 and args.stagger_groups > 1:
+            line["staggered"] = staggered(args, solver, inputs, args.stagger_groups)
         if world == 1 and not args.no_warm:
             line["warm"] = warm_ticks(solver, inputs, nenv, args.steps, args.warmup,
                                       shard_seed(rank) + 7, stream)

@@ -211,10 +211,13 @@ int osc_batch_solve(const osc_model* model, int32_t nenv,
  * variables y = (u, z)) into `workspace`; osc_batch_solve_assembled runs the interior-point solve
  * on it and writes the outputs exactly as osc_batch_solve does (contact_mask must be the one
  * assembled with).  Here `workspace` is required (>= osc_workspace_bytes, 16-byte aligned).  Its
- * layout per environment, in doubles: [g (NY, padded even) | Hr (NY x NY, padded
- * even) | X (nv x (NY+1), row stride padded even) | H_dv (nv x nv) | f_dv (nv, padded even) |
- * solver hand-off], stride osc_workspace_env_bytes, with dv = X [y; 1] = M^-1 (B u + Jc z - C),
+ * layout per environment, in doubles: [g (NY, padded even) | Hr (padded even) | X
+ * (nv x (NY+1), row stride padded even) | H_dv (nv x nv) | f_dv (nv, padded even) | solver
+ * hand-off], stride osc_workspace_env_bytes, with dv = X [y; 1] = M^-1 (B u + Jc z - C),
  * H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t) (wheel rows: further blocks).
+ * Hr (symmetric) is stored compact (round 6) -- its rows 16 .. NY-1 whole (row-major, NY columns
+ * each), then the upper triangle of its leading 16 x 16 block packed row by row: (NY-16) NY + 136
+ * doubles -- except for models with wheel rows, which keep the full NY x NY row-major Hr.
  * The solve WRITES to the workspace: its per-env hand-off blocks and, past the reduced QPs, the
  * solve-status scratch, the lockstep compaction's park area, slot list and counter
  * -- one workspace serves one solve at a time; concurrent solves on several streams need a

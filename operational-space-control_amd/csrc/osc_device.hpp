@@ -99,9 +99,19 @@ struct Dims {
   static_assert(NB >= 1 && NB <= 8, "floating-base block");
 
   // ---- workspace per env (doubles): [g | Hr | X | H_dv | f_dv | W_SOL] ----
+  // Hr (symmetric, exactly) is stored COMPACT without wheel rows (round 6):
+  // [A = its rows 16 .. NY-1, all NY columns, row-major | T = the upper triangle of its leading
+  // 16 x 16 block, packed row-major] -- (NY - 16) NY + 136 doubles instead of NY^2 (Go2 328 vs
+  // 576, WaLTER 648 vs 1,024): what the interior point streams each iteration (the second column
+  // slot = rows 16.. by symmetry) stays whole rows; hr_off() maps (i, j) into it.  Wheel models
+  // keep the full row-major Hr (their rotated Newton systems read it by columns).
+  static constexpr bool HRC = !WH;
+  static constexpr int HRA = NY - kRow;                 // rows in A
+  static constexpr int HR_T = HRA * NY;                 // T's offset in the block
+  static constexpr int HR_SIZE = HRC ? HR_T + kRow * (kRow + 1) / 2 : NY * NY;
   static constexpr int W_G = 0;
   static constexpr int W_HR = even(NY);
-  static constexpr int W_X = W_HR + even(NY * NY);
+  static constexpr int W_X = W_HR + even(HR_SIZE);
   // H_dv = 2 J'WJ + 2 w_reg I and f_dv = 2 J'W (b - t), for the full-space refinement after the
   // interior point (its gradient never goes through Hr)
   static constexpr int W_HD = W_X + NV * NY1P;
@@ -171,6 +181,19 @@ struct Dims {
 
 };
 
+// Offset of Hr[i][j] in the workspace's Hr block (Dims::HRC: the compact layout above).
+template <class D>
+__host__ __device__ constexpr int hr_off(int i, int j) {
+  if constexpr (!D::HRC) {
+    return i * D::NY + j;
+  } else {
+    if (i >= kRow) return (i - kRow) * D::NY + j;
+    if (j >= kRow) return (j - kRow) * D::NY + i;
+    const int a = i < j ? i : j, b = i < j ? j : i;
+    return D::HR_T + a * kRow - a * (a - 1) / 2 + (b - a);
+  }
+}
+
 // ---- IPM-kernel LDS per env (doubles): workspace prefix [g (| Hr)] + vectors.
 // Large batches (two waves per SIMD): Hr is NOT in LDS -- each lane streams its two Hr columns
 // from the L2-resident workspace into the Newton-matrix registers once per iteration, which
@@ -181,9 +204,11 @@ template <class D, bool HRL>
 struct IpmLayout {
   static constexpr int NY = D::NY, NU = D::NU, NC = D::NC, NB = D::NB;
   static constexpr int I_G = D::W_G;
-  static constexpr int I_HR = D::W_HR;                 // valid when HRL
-  static constexpr int STAGE = HRL ? D::W_X : D::W_HR; // workspace prefix copied to LDS
-  static constexpr int I_VY = STAGE;                   // y (current iterate)
+  static constexpr int I_HR = D::W_HR;                 // valid when HRL: full NY x NY, row-major
+  // workspace prefix copied to LDS as it stands: [g | Hr] where the workspace's Hr is full,
+  // [g] alone where it is compact (HRL then expands Hr into its full LDS layout, osc_ipm.hpp)
+  static constexpr int STAGE = (HRL && !D::HRC) ? D::W_X : D::W_HR;
+  static constexpr int I_VY = HRL ? D::W_HR + even(NY * NY) : D::W_HR;   // y (current iterate)
   static constexpr int I_VY2 = I_VY + even(NY);        // search direction
   static constexpr int I_UV = I_VY2 + even(NY);        // (unused slot: keeps the layout fixed)
   static constexpr int I_VR = I_UV + even(NU);         // a row-space vector

@@ -373,6 +373,38 @@ __device__ __forceinline__ void ipm_block(
     if (l < NC) sMask[l] = mk;
   }
   const double* sHr = B + LY::I_HR;
+  if constexpr (HRL && D::HRC) {   // the workspace's compact Hr -> its full LDS layout, once
+    const int ca = l, cb = l + kRow < NY ? l + kRow : NY - 1;   // this lane's two columns
+    // fused refinement: the compact block is copied whole (16-byte loads) into the refinement's
+    // LDS region -- free until the [H_dv | f_dv] DMA of the refinement -- and expanded from there
+    // (per-lane addresses into LDS, not into L2); otherwise read from the workspace directly
+    const double* src = wsw + lane_off;
+    if constexpr (kXinHr) {
+      static_assert(D::HR_SIZE % 2 == 0 && D::HR_SIZE <= refine_lds_extra<D, SMALL, RF>() &&
+                    D::W_HR % 2 == 0, "compact Hr staged in the refinement region");
+      Batch2<D::HR_SIZE / 2, kRow> bh;
+      bh.load(ws + static_cast<size_t>(env) * D::WS + D::W_HR, l);
+      bh.store(B + LY::IL, l);
+      wave_sync();
+      src = B + LY::IL;
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < NY; i0 += 8) {
+      double hv0[8], hv1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        hv0[i] = i0 + i < NY ? src[hr_off<D>(i0 + i, ca)] : 0.0;
+        hv1[i] = i0 + i < NY ? src[hr_off<D>(i0 + i, cb)] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i0 + i < NY) {
+          const_cast<double*>(sHr)[(i0 + i) * NY + ca] = hv0[i];
+          if (l + kRow < NY) const_cast<double*>(sHr)[(i0 + i) * NY + cb] = hv1[i];
+        }
+      }
+    }
+  }
   if constexpr (HRH) {   // Hr's first column slot, once per solve
     static_assert(NY % 2 == 0 && D::WS % 2 == 0 && D::W_HR % 2 == 0, "16-byte Hr row loads");
 #pragma unroll
@@ -380,7 +412,7 @@ __device__ __forceinline__ void ipm_block(
       double hv[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        hv[i] = i0 + i < NY ? wsw[lane_off + static_cast<unsigned>((i0 + i) * NY + l)] : 0.0;
+        hv[i] = i0 + i < NY ? wsw[lane_off + static_cast<unsigned>(hr_off<D>(i0 + i, l))] : 0.0;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (i0 + i < NY) sHh[(i0 + i) * kRow + l] = hv[i];
@@ -647,8 +679,8 @@ __device__ __forceinline__ void ipm_block(
   if constexpr (kHrReg) {
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
-      hr0[i] = wsw[lane_off + static_cast<unsigned>(i * NY + j0)];
-      hr1[i] = wsw[lane_off + static_cast<unsigned>(i * NY + jj1)];
+      hr0[i] = wsw[lane_off + static_cast<unsigned>(hr_off<D>(i, j0))];
+      hr1[i] = wsw[lane_off + static_cast<unsigned>(hr_off<D>(i, jj1))];
     }
   }
   // Hr columns j0, j1 (and their diagonal entries) -> registers; re-issued at the end of every
@@ -672,7 +704,7 @@ __device__ __forceinline__ void ipm_block(
       unsigned off = lane_off;
       asm volatile("" : "+v"(off));
       // column jj1 = row jj1: this lane's contiguous NY doubles, two per 16-byte load
-      const double* p1 = wsw + off + jj1 * NY;
+      const double* p1 = wsw + off + hr_off<D>(jj1, 0);   // (row jj1 of A when compact)
 #pragma unroll
       for (int i = 0; i < NY; ++i) c1[i] = p1[i];
 #pragma unroll
@@ -680,18 +712,18 @@ __device__ __forceinline__ void ipm_block(
     } else {
       unsigned off = lane_off;
       asm volatile("" : "+v"(off));
-      const double* p0 = wsw + off + j0;
-      const double* p1 = wsw + off + jj1;
+      const double* p = wsw + off;
 #pragma unroll
       for (int i = 0; i < NY; ++i) {
-        c0[i] = p0[i * NY];
-        c1[i] = p1[i * NY];
+        c0[i] = p[hr_off<D>(i, j0)];
+        c1[i] = p[hr_off<D>(i, jj1)];
       }
     }
   };
-  const double hdg0 = HRL ? sHr[j0 * NY + j0] : wsw[lane_off + static_cast<unsigned>(j0 * NY + j0)];
+  const double hdg0 =
+      HRL ? sHr[j0 * NY + j0] : wsw[lane_off + static_cast<unsigned>(hr_off<D>(j0, j0))];
   const double hdg1 =
-      HRL ? sHr[jj1 * NY + jj1] : wsw[lane_off + static_cast<unsigned>(jj1 * NY + jj1)];
+      HRL ? sHr[jj1 * NY + jj1] : wsw[lane_off + static_cast<unsigned>(hr_off<D>(jj1, jj1))];
   load_hr();
   const double g0 = sG[j0], g1 = sG[jj1];
   double y0 = 0.0, y1 = 0.0;
@@ -1233,8 +1265,8 @@ __device__ __forceinline__ void ipm_block(
             // Hr's LDS region holds X now: Hr columns from the (L2-resident) workspace
 #pragma unroll
             for (int i = 0; i < NY; ++i) {
-              c0[i] = wsw[lane_off + static_cast<unsigned>(i * NY + j0)];
-              c1[i] = wsw[lane_off + static_cast<unsigned>(i * NY + jj1)];
+              c0[i] = wsw[lane_off + static_cast<unsigned>(hr_off<D>(i, j0))];
+              c1[i] = wsw[lane_off + static_cast<unsigned>(hr_off<D>(i, jj1))];
             }
           } else {
             load_hr();

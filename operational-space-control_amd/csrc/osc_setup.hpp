@@ -819,6 +819,19 @@ __device__ __forceinline__ void setup_env(
     const double wu2 = 2.0 * (P->w_torque + P->w_reg);
     const double wr2 = 2.0 * P->w_reg;
     double* wsv = ws + static_cast<size_t>(env) * D::WS;   // [Hr | g] out from registers
+    // Hr[a][b] = Hr[b][a] = v (a <= b) in the workspace's Hr layout (hr_off: compact without wheel
+    // rows -- rows 16.. whole, the leading 16 x 16 block as a packed triangle)
+    auto store_hr = [&](int a, int b, double v) {
+      if constexpr (!D::HRC) {
+        wsv[D::W_HR + a * NY + b] = v;
+        wsv[D::W_HR + b * NY + a] = v;
+      } else if (b >= kRow) {
+        wsv[D::W_HR + hr_off<D>(b, a)] = v;                       // row b of A
+        if (a >= kRow && a != b) wsv[D::W_HR + hr_off<D>(a, b)] = v;   // row a of A
+      } else {
+        wsv[D::W_HR + hr_off<D>(a, b)] = v;                       // the triangle
+      }
+    };
     constexpr int NT = CB * (CB + 1) / 2;   // upper block triangle, tiles interleaved per k-step
     d4 hacc[NT];
 #pragma unroll
@@ -858,13 +871,11 @@ __device__ __forceinline__ void setup_env(
                 wab = fma(wi * sT[a * D::WTST + i], sT[b * D::WTST + i], wab);
               }
               v += wab;
-              wsv[D::W_HR + a * NY + b] = v;
-              wsv[D::W_HR + b * NY + a] = v;
+              store_hr(a, b, v);
             } else if (b < NY) {
               if (a == b && a < NU) v += wu2;
               if (a == b && a >= NU) v = (mk == 0.0) ? 1.0 : v + wr2;   // pinned z: identity row
-              wsv[D::W_HR + a * NY + b] = v;
-              wsv[D::W_HR + b * NY + a] = v;
+              store_hr(a, b, v);
             } else {
               wsv[D::W_G + a] = v;
             }

@@ -16,8 +16,11 @@
 #   pmc=<robot>:<nenv>         FETCH_SIZE and WRITE_SIZE passes (separate runs) of one batch
 #   sq=<robot>:<nenv>          SQ issue counters of one batch
 #   ab=<old.so>                tools/ab_time.py <old.so> vs the in-tree library (AB_* env)
+#   rocab=<lib.so>:<robot>:<nenv>  one library's cold solves under rocprofv3 --kernel-trace --stats
+#                              -> rocab_<n>/ (per-kernel durations of an A/B side)
 #   hostfed                    bench's host_fed object alone (4,096 and 8,192 envs)
 #   py=<script args>           python <script args>       -> py_<n>.log
+#   exe=<program args>         a built tool (tools/bin/...) -> exe_<n>.log
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
@@ -65,11 +68,17 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_ANY -d "$P/pmc_cyc" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/sq.err" || exit $((30 + n)) ;;
     ab)
       timeout -k 10 500 python tools/ab_time.py "$val" operational-space-control_amd/lib/libosc_batch.so > "$O/ab_$n.jsonl" 2>&1 || exit $((30 + n)) ;;
+    rocab)
+      lib=${val%%:*}; rest=${val#*:}
+      AB_CONFIGS="$rest" AB_ONLY="$rest" AB_ROUNDS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/rocab_$n" -o run --output-format csv -- python3 tools/ab_time.py "$lib" > "$O/rocab_$n.jsonl" 2>&1 || exit $((30 + n)) ;;
     hostfed)
       timeout -k 10 300 python bench.py --no-cpu --no-front-end --no-single-env --no-north-star --no-mixed --hbm-batches 0 --no-warm > "$O/bench_hostfed.json" 2> "$O/bench_hostfed.err" || exit $((30 + n)) ;;
     py)
       # shellcheck disable=SC2086
       timeout -k 10 600 python -u $val > "$O/py_$n.log" 2>&1 || exit $((30 + n)) ;;
+    exe)
+      # shellcheck disable=SC2086
+      timeout -k 10 120 $val > "$O/exe_$n.log" 2>&1 || exit $((30 + n)) ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

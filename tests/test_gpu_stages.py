@@ -24,6 +24,21 @@ from osc_qp import b_matrix, build_qp, contact_jacobian, load_model
 pytestmark = pytest.mark.gpu
 
 
+def unpack_hr(block, ny):
+    """The workspace's compact Hr (include/osc_batch.h): A = rows 16..ny-1 (ny columns each),
+    then T = the upper triangle of Hr[0:16, 0:16] row by row."""
+    Hr = np.zeros((ny, ny))
+    A = block[:(ny - 16) * ny].reshape(ny - 16, ny)
+    Hr[16:, :] = A
+    Hr[:, 16:] = A.T
+    t = (ny - 16) * ny
+    for a in range(16):
+        Hr[a, a:16] = block[t:t + 16 - a]
+        Hr[a:16, a] = block[t:t + 16 - a]
+        t += 16 - a
+    return Hr
+
+
 @pytest.mark.parametrize("robot,mask_mode", [("unitree_go2", "bernoulli"), ("walter_sr", "bernoulli"),
                                              ("unitree_go2", "zeros")])
 def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
@@ -50,7 +65,10 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     ty = True
     nxr = nv if ty else nb
     o_hr = o_u + (0 if ty else nu * ny1p)
-    o_x = o_hr + ev(ny * ny)
+    # Hr compact (round 6; osc_device.hpp hr_off): rows 16.. whole, then the leading 16 x 16
+    # block's upper triangle packed row-major
+    hr_size = (ny - 16) * ny + 16 * 17 // 2
+    o_x = o_hr + ev(hr_size)
     o_hd = o_x + nxr * ny1p
     o_gd = o_hd + nv * nv
     nrl = (2 * nu + 6 * nc + 15) // 16
@@ -65,7 +83,7 @@ def test_reduced_qp_consistent_with_oracle_qp(gpu, robot, mask_mode):
     model = load_model(robot)
     rng = np.random.default_rng(0)
     for e in range(nenv):
-        Hr = D[e, o_hr:o_hr + ny * ny].reshape(ny, ny)
+        Hr = unpack_hr(D[e, o_hr:o_hr + hr_size], ny)
         g = D[e, o_g:o_g + ny]
         U = np.eye(nu, ny + 1) if ty else D[e, o_u:o_hr].reshape(nu, ny1p)[:, :ny + 1]
         X = D[e, o_x:o_hd].reshape(nxr, ny1p)[:, :ny + 1]
