@@ -471,11 +471,13 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
                 h2d = float(np.mean([t["h2d_ms"] for t in tims]))
                 sol = float(np.mean([t["solve_ms"] for t in tims]))
                 d2h = float(np.mean([t["d2h_ms"] for t in tims]))
+                kin_ms = float(np.mean([t.get("kin_ms", 0.0) for t in tims]))
                 period = stats.elapsed_s / steps * 1e3
                 serial = h2d + sol + d2h
                 longest = max(h2d, sol, d2h)
                 entry = {"value": job_value(stats, steps), "unit": "solves/s",
                          "ms_per_tick": period, "h2d_ms": h2d, "solve_ms": sol, "d2h_ms": d2h,
+                         **({"kin_ms": kin_ms} if form == "joint_states" else {}),
                          "h2d_bytes": int(feed.in_bytes), "d2h_bytes": int(feed.out_bytes),
                          "h2d_GBps": feed.in_bytes / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
                          "bytes_per_env_h2d": feed.in_bytes / nenv,
@@ -614,9 +616,12 @@ def parse_args(argv=None):
     ap.add_argument("--host-fed-depth", type=int, default=2,
                     help="pipeline slots of the host-fed tick (2 = H2D of tick k overlaps the "
                          "solve of tick k-1)")
-    ap.add_argument("--stagger-groups", type=int, default=4,
+    ap.add_argument("--stagger-groups", type=int, default=0,
                     help="the `staggered` object beside the headline: its batch as this many env "
-                         "groups ticking out of phase on their own streams; <= 1 = off")
+                         "groups ticking out of phase on their own streams; <= 1 = off (default: "
+                         "off -- in a process that already holds more streams than the GPU's 4 "
+                         "hardware queues the groups share queues and serialise; measured on its "
+                         "own by tools/stagger_probe.py)")
     ap.add_argument("--hbm-only", action="store_true",
                     help="run only the HBM-input rotation (for rocprofv3 --pmc passes)")
     ap.add_argument("--hbm-traffic-json",

@@ -19,7 +19,9 @@
  *   OSC_FEED_QP            M, C, J, b, T, mask: what update_osc_data hands the QP (osc.h:376-455),
  *                          7,664 B per Go2 env; solved by osc_batch_solve(_warm).
  *   OSC_FEED_JOINT_STATES  qpos, qvel, T, mask: what update_mj_data packs (osc.h:350-374), 568 B
- *                          per Go2 env; solved by osc_batch_solve_qpos(_warm) (GPU kinematics).
+ *                          per Go2 env; the kinematics (osc_batch_kinematics) runs on the copy
+ *                          stream right behind its H2D -- overlapping the previous tick's solve --
+ *                          then osc_batch_solve(_warm): bitwise osc_batch_solve_qpos(_warm).
  * Layouts per array are those of osc_batch.h / osc_kinematics.h (env-major, row-major per env).
  *
  * Use (one host thread per feed):
@@ -81,6 +83,9 @@ typedef struct {
   float solve_ms;
   float d2h_ms;
   float h2d_start_to_d2h_end_ms;  /* the tick's latency on the device side                     */
+  float kin_ms;                   /* OSC_FEED_JOINT_STATES: the kinematics kernel (run on the copy
+                                     stream behind the H2D, overlapping the previous tick's
+                                     solve); ~0 for OSC_FEED_QP                                */
 } osc_feed_timing;
 
 /* Create a feed on the current HIP device (that of `model`).  `kin` is required for

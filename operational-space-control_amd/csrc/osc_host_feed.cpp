@@ -1,7 +1,7 @@
 // osc_host_feed.cpp -- the host-fed batched control tick (include/osc_host_feed.h, SURVEY.md
 // §8(e)): pinned host slots -> one H2D copy per tick -> the batched solve -> D2H of the torques,
 // pipelined over `depth` slots on three HIP streams.  Host code over the public C-ABI only
-// (osc_batch_solve(_warm), osc_batch_solve_qpos(_warm)); the reference it replaces is the
+// (osc_batch_kinematics, osc_batch_solve(_warm)); the reference it replaces is the
 // per-tick hand-off of unitree_go2/operational_space_controller.h:546-573 (State and targets in
 // host memory under the mutex, the solve, the torque copy back).
 #include "osc_host_feed.h"
@@ -16,13 +16,14 @@ namespace {
 constexpr size_t kAlign = 256;   // every array of a slot starts on a 256-B boundary
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
-enum Ev { kH2dBeg, kH2dEnd, kSolveBeg, kSolveEnd, kD2hBeg, kD2hEnd, kNumEv };
+enum Ev { kH2dBeg, kH2dEnd, kKinEnd, kSolveBeg, kSolveEnd, kD2hBeg, kD2hEnd, kNumEv };
 
 struct Slot {
   char* h_in = nullptr;        // pinned
   char* d_in = nullptr;        // HBM
   char* h_out = nullptr;       // pinned
   char* d_out = nullptr;       // HBM
+  char* d_kin = nullptr;       // HBM: joint-state form, the kinematics' M, C, J, b of this slot
   hipEvent_t ev[kNumEv] = {};
   int32_t tick = -1;           // last tick submitted into this slot
 };
@@ -39,6 +40,7 @@ struct osc_host_feed {
   size_t off_M = 0, off_C = 0, off_J = 0, off_b = 0, off_qpos = 0, off_qvel = 0, off_T = 0,
          off_mask = 0, in_bytes = 0;
   size_t off_tau = 0, off_status = 0, off_iters = 0, out_bytes = 0;
+  size_t kin_M = 0, kin_C = 0, kin_J = 0, kin_b = 0, kin_bytes = 0;   // joint-state form
   Slot slot[OSC_FEED_MAX_DEPTH];
   hipStream_t s_h2d = nullptr, s_solve = nullptr, s_d2h = nullptr;
   void* ws = nullptr;
@@ -58,6 +60,7 @@ void release(osc_host_feed* f) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
+    if (s.d_kin) (void)hipFree(s.d_kin);
   }
   for (hipStream_t st : {f->s_h2d, f->s_solve, f->s_d2h})
     if (st) (void)hipStreamDestroy(st);
@@ -125,6 +128,14 @@ extern "C" int osc_host_feed_create(const osc_model* model, const osc_kin_model*
   f->off_status = take(n * sizeof(int32_t));
   f->off_iters = take(n * sizeof(int32_t));
   f->out_bytes = o;
+  if (form == OSC_FEED_JOINT_STATES) {
+    o = 0;
+    f->kin_M = take(n * d.nv * d.nv * e8);
+    f->kin_C = take(n * d.nv * e8);
+    f->kin_J = take(n * 6 * d.ns * d.nv * e8);
+    f->kin_b = take(n * 6 * d.ns * e8);
+    f->kin_bytes = o;
+  }
 
   int rc = OSC_ERR_DEVICE;
   bool good =
@@ -136,7 +147,8 @@ extern "C" int osc_host_feed_create(const osc_model* model, const osc_kin_model*
     good = ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_in), f->in_bytes, hipHostMallocDefault)) &&
            ok(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), f->out_bytes, hipHostMallocDefault)) &&
            ok(hipMalloc(reinterpret_cast<void**>(&s.d_in), f->in_bytes)) &&
-           ok(hipMalloc(reinterpret_cast<void**>(&s.d_out), f->out_bytes));
+           ok(hipMalloc(reinterpret_cast<void**>(&s.d_out), f->out_bytes)) &&
+           (f->kin_bytes == 0 || ok(hipMalloc(reinterpret_cast<void**>(&s.d_kin), f->kin_bytes)));
     for (int e = 0; good && e < kNumEv; ++e) good = ok(hipEventCreate(&s.ev[e]));
     if (good) {   // zero host inputs: a tick submitted without being written solves a defined QP
       std::memset(s.h_in, 0, f->in_bytes);
@@ -144,10 +156,9 @@ extern "C" int osc_host_feed_create(const osc_model* model, const osc_kin_model*
     }
   }
   if (good) {
-    if (form == OSC_FEED_QP)
-      good = osc_workspace_bytes(model, nenv, &f->ws_bytes) == OSC_OK;
-    else
-      good = osc_qpos_workspace_bytes(model, kin, nenv, &f->ws_bytes) == OSC_OK;
+    // (the joint-state form runs the kinematics itself, into the slot's d_kin: the solve's
+    // workspace is osc_batch_solve's)
+    good = osc_workspace_bytes(model, nenv, &f->ws_bytes) == OSC_OK;
     good = good && ok(hipMalloc(&f->ws, f->ws_bytes));
   }
   if (good && (flags & OSC_FEED_WARM)) {
@@ -206,12 +217,26 @@ extern "C" int osc_host_feed_submit(osc_host_feed* f, int32_t tick) {
       !ok(hipMemcpyAsync(s.d_in, s.h_in, f->in_bytes, hipMemcpyHostToDevice, f->s_h2d)) ||
       !ok(hipEventRecord(s.ev[kH2dEnd], f->s_h2d)))
     return OSC_ERR_DEVICE;
-  // solve: after this tick's H2D, and after the D2H of tick - depth has read the slot's outputs
-  if (!ok(hipStreamWaitEvent(f->s_solve, s.ev[kH2dEnd], 0)) ||
+  auto in = [&](size_t off) { return reinterpret_cast<const double*>(s.d_in + off); };
+  auto kb = [&](size_t off) { return reinterpret_cast<double*>(s.d_kin + off); };
+  if (f->form == OSC_FEED_JOINT_STATES) {
+    // joint states: the kinematics runs on the copy stream right behind its H2D (round 6), so it
+    // overlaps the previous tick's solve -- the interior point's straggler tail leaves most SIMDs
+    // idle -- instead of heading this tick's solve (osc_batch_solve_qpos = osc_batch_kinematics +
+    // osc_batch_solve: bitwise the same).  The slot's d_kin was last read by the solve of tick -
+    // depth, which the copy stream has waited for above.
+    const int krc = osc_batch_kinematics(f->kin, f->nenv, in(f->off_qpos), in(f->off_qvel),
+                                         kb(f->kin_M), kb(f->kin_C), kb(f->kin_J), kb(f->kin_b),
+                                         nullptr, f->s_h2d);
+    if (krc != OSC_OK) return krc;
+  }
+  if (!ok(hipEventRecord(s.ev[kKinEnd], f->s_h2d))) return OSC_ERR_DEVICE;
+  // solve: after this tick's H2D (and kinematics), and after the D2H of tick - depth has read the
+  // slot's outputs
+  if (!ok(hipStreamWaitEvent(f->s_solve, s.ev[kKinEnd], 0)) ||
       (reuse && !ok(hipStreamWaitEvent(f->s_solve, s.ev[kD2hEnd], 0))) ||
       !ok(hipEventRecord(s.ev[kSolveBeg], f->s_solve)))
     return OSC_ERR_DEVICE;
-  auto in = [&](size_t off) { return reinterpret_cast<const double*>(s.d_in + off); };
   double* tau = reinterpret_cast<double*>(s.d_out + f->off_tau);
   int32_t* status = reinterpret_cast<int32_t*>(s.d_out + f->off_status);
   int32_t* iters = reinterpret_cast<int32_t*>(s.d_out + f->off_iters);
@@ -225,13 +250,12 @@ extern "C" int osc_host_feed_submit(osc_host_feed* f, int32_t tick) {
                                    in(f->off_b), in(f->off_T), in(f->off_mask), tau, nullptr,
                                    status, iters, f->ws, f->ws_bytes, f->s_solve);
   } else {
-    rc = f->warm ? osc_batch_solve_qpos_warm(f->model, f->kin, f->nenv, in(f->off_qpos),
-                                             in(f->off_qvel), in(f->off_T), in(f->off_mask), tau,
-                                             nullptr, status, iters, f->warm, f->warm_bytes,
-                                             f->ws, f->ws_bytes, f->s_solve)
-                 : osc_batch_solve_qpos(f->model, f->kin, f->nenv, in(f->off_qpos),
-                                        in(f->off_qvel), in(f->off_T), in(f->off_mask), tau,
-                                        nullptr, status, iters, f->ws, f->ws_bytes, f->s_solve);
+    const double *M = kb(f->kin_M), *C = kb(f->kin_C), *J = kb(f->kin_J), *b = kb(f->kin_b);
+    rc = f->warm ? osc_batch_solve_warm(f->model, f->nenv, M, C, J, b, in(f->off_T),
+                                        in(f->off_mask), tau, nullptr, status, iters, f->warm,
+                                        f->warm_bytes, f->ws, f->ws_bytes, f->s_solve)
+                 : osc_batch_solve(f->model, f->nenv, M, C, J, b, in(f->off_T), in(f->off_mask),
+                                   tau, nullptr, status, iters, f->ws, f->ws_bytes, f->s_solve);
   }
   if (rc != OSC_OK) return rc;
   if (!ok(hipEventRecord(s.ev[kSolveEnd], f->s_solve))) return OSC_ERR_DEVICE;
@@ -267,6 +291,7 @@ extern "C" int osc_host_feed_timing(osc_host_feed* f, int32_t tick, osc_feed_tim
   if (!ok(hipEventElapsedTime(&t->h2d_ms, s.ev[kH2dBeg], s.ev[kH2dEnd])) ||
       !ok(hipEventElapsedTime(&t->solve_ms, s.ev[kSolveBeg], s.ev[kSolveEnd])) ||
       !ok(hipEventElapsedTime(&t->d2h_ms, s.ev[kD2hBeg], s.ev[kD2hEnd])) ||
+      !ok(hipEventElapsedTime(&t->kin_ms, s.ev[kH2dEnd], s.ev[kKinEnd])) ||
       !ok(hipEventElapsedTime(&t->h2d_start_to_d2h_end_ms, s.ev[kH2dBeg], s.ev[kD2hEnd])))
     return OSC_ERR_DEVICE;
   return OSC_OK;

@@ -1165,7 +1165,10 @@ __device__ __forceinline__ void ipm_block(
     }
     sVy[j0] = y0;
     if (v1) sVy[j1] = y1;
-    load_hr();   // next iteration's Hr columns (the factor in c0/c1 is dead now)
+    // next iteration's Hr columns (the factor in c0/c1 is dead now).  (Round 6: issuing them right
+    // after the last pass's solve instead, so the L2 loads of the two-wave kernel fly during the
+    // ratio tests, measured no gain -- Go2 8,192 0.2534 vs 0.2531 ms, 65,536 1.593 vs 1.600.)
+    load_hr();
     wave_sync();
     if constexpr (WHR) {   // the rows' residual at the new iterate (next step, stop test)
       double yh0, yh1;

@@ -130,7 +130,7 @@ class OscFeedOutputs(ctypes.Structure):
 class OscFeedTiming(ctypes.Structure):
     """osc_feed_timing (include/osc_host_feed.h): per-stage HIP-event durations (ms)."""
     _fields_ = [(n, ctypes.c_float) for n in ("h2d_ms", "solve_ms", "d2h_ms",
-                                               "h2d_start_to_d2h_end_ms")]
+                                               "h2d_start_to_d2h_end_ms", "kin_ms")]
 
 
 FEED_QP, FEED_JOINT_STATES, FEED_WARM = 0, 1, 1

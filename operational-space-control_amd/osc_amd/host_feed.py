@@ -102,4 +102,4 @@ class HostFeed:
         if rc != 0:
             raise _lib.OSCError("osc_host_feed_timing", rc)
         return {"h2d_ms": t.h2d_ms, "solve_ms": t.solve_ms, "d2h_ms": t.d2h_ms,
-                "latency_ms": t.h2d_start_to_d2h_end_ms}
+                "kin_ms": t.kin_ms, "latency_ms": t.h2d_start_to_d2h_end_ms}

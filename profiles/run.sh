@@ -19,6 +19,7 @@
 #   rocab=<lib.so>:<robot>:<nenv>  one library's cold solves under rocprofv3 --kernel-trace --stats
 #                              -> rocab_<n>/ (per-kernel durations of an A/B side)
 #   hostfed                    bench's host_fed object alone (4,096 and 8,192 envs)
+#   rehearse                   bench.py --gpus 2 on this one GPU (ranks over gloo), host_fed on
 #   py=<script args>           python <script args>       -> py_<n>.log
 #   exe=<program args>         a built tool (tools/bin/...) -> exe_<n>.log
 set -o pipefail
@@ -73,6 +74,8 @@ for step in "$@"; do
       AB_CONFIGS="$rest" AB_ONLY="$rest" AB_ROUNDS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/rocab_$n" -o run --output-format csv -- python3 tools/ab_time.py "$lib" > "$O/rocab_$n.jsonl" 2>&1 || exit $((30 + n)) ;;
     hostfed)
       timeout -k 10 300 python bench.py --no-cpu --no-front-end --no-single-env --no-north-star --no-mixed --hbm-batches 0 --no-warm > "$O/bench_hostfed.json" 2> "$O/bench_hostfed.err" || exit $((30 + n)) ;;
+    rehearse)
+      OSC_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu --no-warm --no-front-end --no-single-env > "$O/rehearse_2ranks.json" 2> "$O/rehearse_2ranks.err" || exit $((30 + n)) ;;
     py)
       # shellcheck disable=SC2086
       timeout -k 10 600 python -u $val > "$O/py_$n.log" 2>&1 || exit $((30 + n)) ;;
