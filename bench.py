@@ -430,10 +430,17 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
              for k in range(2)]
         qs = [random_states(tree, nenv, shard_seed(rank) + 50 + k, joint_range=0.5)
               for k in range(2)]
-        for form in ("qp", "joint_states"):
+        # the warm-started loop (the reference warm-starts every tick, osc.h:519-526): two joint
+        # states one control step apart (joint angles +-0.01 rad, velocities +-1 %), alternating
+        rng = np.random.default_rng(shard_seed(rank) + 60)
+        q1, v1 = qs[0][0].copy(), qs[0][1] * (1.0 + 0.01 * rng.standard_normal(qs[0][1].shape))
+        q1[:, 7:] += 0.01 * rng.standard_normal(q1[:, 7:].shape)
+        qw = [qs[0], (q1, v1)]
+        for key, form, warm in (("qp", "qp", False), ("joint_states", "joint_states", False),
+                                ("joint_states_warm", "joint_states", True)):
             row = {}
             for depth in (args.host_fed_depth, 1):
-                feed = feed_cls(solver, nenv, form, depth=depth,
+                feed = feed_cls(solver, nenv, form, depth=depth, warm=warm,
                                 kin=kin if form == "joint_states" else None)
                 tick = [0]
 
@@ -443,11 +450,12 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
                     if fill:
                         src = d[k % 2]
                         if form == "qp":
-                            for key in ("M", "C", "J", "b"):
-                                v[key][...] = src[key]
+                            for a in ("M", "C", "J", "b"):
+                                v[a][...] = src[a]
                         else:
-                            v["qpos"][...], v["qvel"][...] = qs[k % 2]
-                        v["T"][...], v["mask"][...] = src["T"], src["mask"]
+                            v["qpos"][...], v["qvel"][...] = (qw if warm else qs)[k % 2]
+                        tm = d[0] if warm else src
+                        v["T"][...], v["mask"][...] = tm["T"], tm["mask"]
                     feed.submit(k)
                     if k >= depth - 1:
                         feed.wait(k - depth + 1)
@@ -464,7 +472,7 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
                 elapsed = time.perf_counter() - t0
                 barrier()
                 last = tick[0] - 1
-                tau, status, _ = feed.wait(last)
+                tau, status, iters = feed.wait(last)
                 conv = int((np.asarray(status) == 0).sum())
                 tims = [feed.timing(j) for j in range(max(0, last - depth + 1), last + 1)]
                 stats = reduce_stats(world, dev, nenv, elapsed, 0.0, 0.0, conv)
@@ -482,6 +490,7 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
                          "h2d_GBps": feed.in_bytes / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
                          "bytes_per_env_h2d": feed.in_bytes / nenv,
                          "converged_frac": stats.converged,
+                         "mean_ipm_iters": float(np.asarray(iters).mean()),
                          "global_envs": stats.total_envs}
                 if depth > 1:
                     entry["overlap_frac"] = ((serial - period) / (serial - longest)
@@ -491,7 +500,7 @@ def host_fed(args, world, rank, dev, barrier, solver, feed_cls=None, kin_cls=Non
                 else:
                     row["serial_depth1"] = {k: entry[k] for k in ("value", "ms_per_tick")}
                 feed.close()
-            res["per_gpu"].setdefault(str(nenv), {})[form] = row
+            res["per_gpu"].setdefault(str(nenv), {})[key] = row
     res["note"] = ("overlap_frac = (h2d + solve + d2h - period) / (h2d + solve + d2h - longest "
                    "stage): 1 = every stage but the longest hidden; serial_depth1 = the same "
                    "ticks with one slot (copies and solve in series)")

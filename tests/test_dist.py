@@ -192,12 +192,13 @@ def test_bench_rank_path_two_gloo_ranks(tmp_path):
     hf = line["host_fed"]
     assert hf["depth"] == 2 and set(hf["per_gpu"]) == {"16", "32"}
     for nenv in (16, 32):
-        for form in ("qp", "joint_states"):
+        for form in ("qp", "joint_states", "joint_states_warm"):
             r = hf["per_gpu"][str(nenv)][form]
             assert r["global_envs"] == 2 * nenv and r["converged_frac"] == 1.0
             assert r["h2d_GBps"] > 0 and r["bound"] == "h2d (PCIe)"
             assert r["value"] > 0 and r["serial_depth1"]["value"] > 0
             assert r["bytes_per_env_h2d"] == (7664 - 96 if form == "qp" else (19 + 18 + 30 + 4) * 8)
+            assert r["mean_ipm_iters"] == 10.0
 
 
 def test_bench_launcher(monkeypatch):
