@@ -622,6 +622,12 @@ def parse_args(argv=None):
     ap.add_argument("--host-fed-envs", default="4096,8192",
                     help="per-GPU batches of the host_fed object (SURVEY.md §8(e): inputs from "
                          "pinned host memory every tick); empty = off")
+    ap.add_argument("--host-fed-after", action="store_true",
+                    help="run the host_fed object after the headline instead of before the "
+                         "north_star / mixed lines (default: before -- like them it completes, "
+                         "synced, before the headline's timed steps, which then start at the "
+                         "clocks of a running loop: Go2 4,096 in the driver's 20 + 5 window 24.1-24.5 "
+                         "vs 23.5-23.8 M solves/s after, profiles/r06/bench_order_ab.jsonl)")
     ap.add_argument("--host-fed-depth", type=int, default=2,
                     help="pipeline slots of the host-fed tick (2 = H2D of tick k overlaps the "
                          "solve of tick k-1)")
@@ -961,19 +967,22 @@ def main(argv=None) -> None:
                                     args.hbm_traffic_json)), flush=True)
         return
     prepared = prepare_headline(args, rank, OSCBatchSolver)
+    # SURVEY.md §8(e)'s host-fed tick: every rank its own pinned feed.  It completes (synced,
+    # barriers) before or after the headline's timed region -- never overlapping it
+    want_hf = bool(args.host_fed_envs.strip()) and args.robot != "mixed"
+    hf = (host_fed(args, world, rank, dev, barrier, prepared[0])
+          if want_hf and not args.host_fed_after else None)
     objs = multi_gpu_objects(args, world, rank, dev, barrier, OSCBatchSolver, clock)
     line, solver, inputs = run_headline(args, world, rank, dev, barrier, OSCBatchSolver, clock,
                                         prepared)
-    # SURVEY.md §8(e)'s host-fed tick: every rank its own pinned feed (after the headline's timed
-    # region, so its PCIe traffic never overlaps it)
-    hf = (host_fed(args, world, rank, dev, barrier, solver)
-          if args.host_fed_envs.strip() and args.robot != "mixed" else None)
+    if want_hf and args.host_fed_after:
+        hf = host_fed(args, world, rank, dev, barrier, solver)
     if line is not None:
         line.update(objs)
         if hf is not None:
             line["host_fed"] = hf
-        line["clocks"] = ("the headline's timed steps run after the north_star / mixed lines "
-                          "(GPU clocks at a running loop's level, not an idle GPU's ramp)")
+        line["clocks"] = ("the headline's timed steps run after the host_fed / north_star / mixed "
+                          "lines (GPU clocks at a running loop's level, not an idle GPU's ramp)")
     if line is not None:
         nenv = args.nenv_per_gpu
         stream = clock.stream()

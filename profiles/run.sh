@@ -15,6 +15,7 @@
 #   configs                    configs[2], [3], Go2 8,192 / 65,536, mixed as bench lines
 #   pmc=<robot>:<nenv>         FETCH_SIZE and WRITE_SIZE passes (separate runs) of one batch
 #   sq=<robot>:<nenv>          SQ issue counters of one batch
+#   pmchbm                     FETCH / WRITE passes of bench --hbm-only (roofline.hbm_inputs)
 #   ab=<old.so>                tools/ab_time.py <old.so> vs the in-tree library (AB_* env)
 #   rocab=<lib.so>:<robot>:<nenv>  one library's cold solves under rocprofv3 --kernel-trace --stats
 #                              -> rocab_<n>/ (per-kernel durations of an A/B side)
@@ -64,6 +65,11 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/trace" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" &&
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$P/pmc_fetch" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" &&
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$P/pmc_write" -o run --output-format csv -- python3 bench.py $A > /dev/null 2>> "$O/pmc.err" || exit $((30 + n)) ;;
+    pmchbm)
+      P="$R/$O/prof_hbm"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/trace" -o run --output-format csv -- python3 bench.py --hbm-only --steps 20 --warmup 5 > /dev/null 2>> "$O/pmc.err" &&
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$P/pmc_fetch" -o run --output-format csv -- python3 bench.py --hbm-only --steps 20 --warmup 5 > /dev/null 2>> "$O/pmc.err" &&
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$P/pmc_write" -o run --output-format csv -- python3 bench.py --hbm-only --steps 20 --warmup 5 > /dev/null 2>> "$O/pmc.err" || exit $((30 + n)) ;;
     sq)
       robot=${val%%:*}; nenv=${val#*:}; P="$R/$O/prof_${robot}_${nenv}"
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_ANY -d "$P/pmc_cyc" -o run --output-format csv -- python3 bench.py --robot "$robot" --nenv-per-gpu "$nenv" --steps 10 --warmup 3 $B > /dev/null 2>> "$O/sq.err" || exit $((30 + n)) ;;
