@@ -103,7 +103,9 @@ int osc_host_feed_inputs(osc_host_feed* feed, int32_t tick, osc_feed_inputs* in)
 
 /* Enqueue tick `tick` (the next one in order): its H2D copy on the copy stream, the solve on the
  * solve stream after it, the D2H of tau / status / iters on the return stream after that.
- * Returns without waiting.  A solve error (osc_batch_solve's argument checks) is returned here. */
+ * Returns without waiting.  A solve error (osc_batch_solve's argument checks) is returned here; an
+ * error past the argument checks leaves the tick half enqueued, so the feed then refuses every
+ * further tick (OSC_ERR_DEVICE) and can only be destroyed. */
 int osc_host_feed_submit(osc_host_feed* feed, int32_t tick);
 
 /* Block until tick `tick`'s outputs are in pinned host memory and return pointers to them.

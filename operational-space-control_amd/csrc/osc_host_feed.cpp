@@ -48,6 +48,7 @@ struct osc_host_feed {
   double* warm = nullptr;
   size_t warm_bytes = 0;
   int32_t next = 0;            // next tick to submit
+  bool failed = false;         // a submit failed part-way: the pipeline state is undefined
 };
 
 namespace {
@@ -185,6 +186,7 @@ extern "C" int osc_host_feed_destroy(osc_host_feed* f) {
 
 extern "C" int osc_host_feed_inputs(osc_host_feed* f, int32_t tick, osc_feed_inputs* in) {
   if (!f || !in || tick != f->next) return OSC_ERR_INVALID_ARGUMENT;
+  if (f->failed) return OSC_ERR_DEVICE;
   Slot& s = f->slot[tick % f->depth];
   // the slot's pinned inputs are free once its previous H2D copy has completed
   if (s.tick >= 0 && !ok(hipEventSynchronize(s.ev[kH2dEnd]))) return OSC_ERR_DEVICE;
@@ -205,10 +207,24 @@ extern "C" int osc_host_feed_inputs(osc_host_feed* f, int32_t tick, osc_feed_inp
   return OSC_OK;
 }
 
+namespace {
+int submit_tick(osc_host_feed* f, int32_t tick);
+}  // namespace
+
 extern "C" int osc_host_feed_submit(osc_host_feed* f, int32_t tick) {
   if (!f || tick != f->next) return OSC_ERR_INVALID_ARGUMENT;
+  if (f->failed) return OSC_ERR_DEVICE;
   int cur = -1;
   if (!ok(hipGetDevice(&cur)) || cur != f->device) return OSC_ERR_INVALID_ARGUMENT;
+  // anything failing past this point leaves part of the tick enqueued: the feed refuses every
+  // further tick (sticky OSC_ERR_DEVICE) and is only good for osc_host_feed_destroy
+  const int rc = submit_tick(f, tick);
+  if (rc != OSC_OK) f->failed = true;
+  return rc;
+}
+
+namespace {
+int submit_tick(osc_host_feed* f, int32_t tick) {
   Slot& s = f->slot[tick % f->depth];
   const bool reuse = s.tick >= 0;
   // H2D: the device inputs of this slot are free once the solve of tick - depth has read them
@@ -269,6 +285,7 @@ extern "C" int osc_host_feed_submit(osc_host_feed* f, int32_t tick) {
   ++f->next;
   return OSC_OK;
 }
+}  // namespace
 
 extern "C" int osc_host_feed_wait(osc_host_feed* f, int32_t tick, osc_feed_outputs* out) {
   if (!f || !out || tick < 0 || tick >= f->next || tick < f->next - f->depth)

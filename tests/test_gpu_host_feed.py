@@ -163,3 +163,24 @@ def _noslip_yaml():
     from osc_amd.robots import config_path
     return os.path.join(os.path.dirname(config_path("walter_sr_wheels")),
                         "walter_sr_wheels_noslip_config.yaml")
+
+
+@pytest.mark.parametrize("nenv", [1, 3])
+def test_tiny_batches(gpu, nenv):
+    """A single env (the reference's own case, configs[0]) and a partial wavefront."""
+    from osc_amd.host_feed import HostFeed
+    from osc_amd.solver import OSCBatchSolver
+    s = OSCBatchSolver("unitree_go2")
+    data = _batches("unitree_go2", nenv, 3, 331)
+    feed = HostFeed(s, nenv, "qp", depth=2)
+    got = {}
+    for k in range(4):
+        if k < 3:
+            _fill(feed, k, data[k])
+            feed.submit(k)
+        if k >= 1:
+            got[k - 1] = feed.wait(k - 1)[0].copy()
+    for k in range(3):
+        r = s.solve(**data[k])
+        torch.cuda.synchronize()
+        assert np.array_equal(got[k], r.tau.cpu().numpy()), k
