@@ -7,17 +7,14 @@ namespace osc {
 
 // one env per 64-lane wavefront (four envs per wavefront measured no faster: Go2 4,096
 // 35.3 vs 33.7 us)
-// (past one round of interior-point waves the lean variant: osc_setup.hpp setup_env's LEAN; it
-// differs only where phase B runs the 2x2-tile loop, i.e. not for the MFMA models)
+// (the models without MFMA assembly -- Go2 -- take the lean variant, osc_setup.hpp setup_env's
+// LEAN, at every batch size: 100 VGPRs and 7.6 KB of LDS fit all of 4,096 envs' waves at once;
+// against the full variant 4,096 / 2,048 -1.8 / -0.1 %, profiles/r06/lean_lds/)
 template <class D>
 void launch_setup(const LaunchArgs& a) {
   const dim3 grid(static_cast<unsigned>(a.nenv));
-  if (!D::JG && a.nenv > a.model->small_batch_max)
-    hipLaunchKernelGGL((osc_setup_kernel<D, !D::JG>), grid, dim3(kWave), 0, a.s, a.model->dparams,
-                       a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
-  else
-    hipLaunchKernelGGL((osc_setup_kernel<D, false>), grid, dim3(kWave), 0, a.s, a.model->dparams,
-                       a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
+  hipLaunchKernelGGL((osc_setup_kernel<D, !D::JG>), grid, dim3(kWave), 0, a.s, a.model->dparams,
+                     a.nenv, a.M, a.C, a.J, a.b, a.T, a.mask, a.ws, a.wdir);
 }
 
 template void launch_setup<Go2>(const LaunchArgs&);

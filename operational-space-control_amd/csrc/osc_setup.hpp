@@ -107,11 +107,12 @@ __device__ __noinline__ void wave_mgs_lds(double* rows, int lane, double drop, d
 // (and, WaLTER, Phase B's J fragments into registers): M, C, J, b never go through HBM.  The
 // kinematics' model tables and per-env state live in the region phases B-D use later (from
 // D::O_HA), so the fused kernel needs kin_lds_doubles<D>() of LDS.
-// LEAN = true (batches past one round of interior-point waves): phase B's 2x2-tile loop unrolled
-// 4 deep instead of fully -- 100 VGPRs instead of 256 (Go2), so three waves share a SIMD; slower
-// where every wave is resident anyway (Go2 4,096: 0.1646 vs 0.1620 ms per solve), faster where the
-// assembly runs many rounds (8,192: 0.2679 vs 0.2701, 65,536: 1.7265 vs 1.7466;
-// profiles/r05/ab_setup_unroll4.jsonl).
+// LEAN = true (Go2's launches, osc_setup.hip): phase B's 2x2-tile loop unrolled 4 deep instead of
+// fully -- 100 VGPRs instead of 256 -- and (kHaG below) Ha kept out of LDS and X laid over A: 7.6
+// instead of 14.2 KB, so 20 waves fit a CU.  Round 5 adopted the unroll for batches past one round
+// of interior-point waves only (4,096: 0.1646 vs 0.1620 ms, when LDS still capped a CU at 11
+// waves; profiles/r05/ab_setup_unroll4.jsonl); with the LDS cut it wins at every size
+// (profiles/r06/lean_lds/).
 template <class D, bool KIN = false, bool LEAN = false>
 __device__ __forceinline__ void setup_env(
     const DevParams* __restrict__ P, int env, int nenv, const double* __restrict__ gM,
@@ -129,10 +130,12 @@ __device__ __forceinline__ void setup_env(
   double* sA = sm + D::O_A;
   double* sM = sm + D::O_M;
   double* sC = sm + D::O_C;
+  // lean assembly without wheel rows: X in Ha's region, phase D's H_dv / f_dv from the workspace
+  constexpr bool kHaG = LEAN && !D::WH && !KIN;
   double* sHa = sm + D::O_HA;
-  double* sX = sm + D::O_X;
-  double* sU = sm + D::O_X + NB * NY1P;   // U parked in X's last rows until X replaces it
-  double* sMask = sm + D::O_MASK;
+  double* sX = sm + (kHaG ? D::O_X_L : D::O_X);
+  double* sU = sX + NB * NY1P;   // U parked in X's last rows until X replaces it
+  double* sMask = sm + (kHaG ? D::O_MASK_L : D::O_MASK);
 
   STAMP_DECL
   STAMP_BEGIN();
@@ -345,8 +348,10 @@ __device__ __forceinline__ void setup_env(
     if (i >= NA || j >= NA) return;
     v *= 2.0;
     if (i == j && i < NV) v += 2.0 * P->w_reg;
-    sHa[i * NA + j] = v;
-    sHa[j * NA + i] = v;
+    if constexpr (!kHaG) {   // (the lean assembly reads H_dv / f_dv back from the workspace)
+      sHa[i * NA + j] = v;
+      sHa[j * NA + i] = v;
+    }
     if (j < NV) {                          // H_dv (i <= j < NV), both triangles
       wha[D::W_HD + i * NV + j] = v;
       wha[D::W_HD + j * NV + i] = v;
@@ -447,6 +452,15 @@ __device__ __forceinline__ void setup_env(
   constexpr int kUStep = kSplitU ? (NU + 1) / 2 : NU;
   const int c = kSplitU ? (lane & 31) : lane;
   const int a_lo = kSplitU ? (lane >> 5) * kUStep : 0;
+  // kHaG: every lane computes its column in registers first and stores it after one barrier -- the
+  // lean assembly's X region overlays A, whose contact rows the columns read.  (The other variants
+  // store as they go: computing first measured 1.6 % slower for WaLTER at 65,536.)
+  double x[NB];
+  double uacc[kUStep];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) x[i] = 0.0;
+#pragma unroll
+  for (int t = 0; t < kUStep; ++t) uacc[t] = 0.0;
   if (c < NY1) {
     const bool pinned = (c >= NU && c < NY) && (sMask[(c - NU) / 3] == 0.0);
     // right-hand side and U's constant term are strided LDS vectors chosen per lane (no
@@ -461,7 +475,6 @@ __device__ __forceinline__ void setup_env(
     const double* up =
         cu ? sM + NB * NV + NB + c : (cz ? sA + (JC0 - JR0 + c - NU) * NAP + NB : sC + NB);
     const double usg = cz ? -1.0 : 1.0;
-    double x[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) x[i] = pinned ? 0.0 : xsg * xp[i * xs];
     // LDL^T of the NB x NB base block (redundantly per lane; NB^3/6 flops)
@@ -495,7 +508,7 @@ __device__ __forceinline__ void setup_env(
     for (int k = NB - 1; k >= 0; --k)
 #pragma unroll
       for (int i = 0; i < k; ++i) x[i] = fma(-L[k][i], x[k], x[i]);
-    if (a_lo == 0) {
+    if (!kHaG && a_lo == 0) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = x[i];
     }
@@ -506,17 +519,22 @@ __device__ __forceinline__ void setup_env(
         double acc = pinned ? 0.0 : usg * up[a * xs];
 #pragma unroll
         for (int i = 0; i < NB; ++i) acc = fma(sM[(NB + a) * NV + i], x[i], acc);
-        sU[a * NY1P + c] = acc;
+        if constexpr (kHaG) uacc[t] = acc;
+        else sU[a * NY1P + c] = acc;
       }
     }
-  } else if (c < NY1P) {   // padding column of X and U: read by the 2x2 tiles, must be 0
+  }
+  if constexpr (kHaG) wave_sync();   // A's contact rows are read: X may overwrite them now
+  // (kHaG: every column; otherwise the padding columns of X and U -- read by the 2x2 tiles -- get
+  // their zeros)
+  if (kHaG ? c < NY1P : (c >= NY1 && c < NY1P)) {
     if (a_lo == 0) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = 0.0;
+      for (int i = 0; i < NB; ++i) sX[i * NY1P + c] = x[i];
     }
 #pragma unroll
     for (int t = 0; t < kUStep; ++t)
-      if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = 0.0;
+      if (a_lo + t < NU) sU[(a_lo + t) * NY1P + c] = uacc[t];
   }
   wave_sync();
   {
@@ -770,6 +788,9 @@ __device__ __forceinline__ void setup_env(
   STAMP_END(2);
   STAMP_BEGIN();
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
+  // (kHaG: H_dv / f_dv come back from the workspace -- this wavefront's own stores of phase B,
+  // complete and visible to its loads after a workgroup-scope fence)
+  if constexpr (kHaG) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   // Hr = X' T1 + 2 (w_tau + w_reg) I_u + 2 w_reg I_z,  g = last column,  T1 = H_dv X (+ f_dv in
   // the affine column).
   {
@@ -794,7 +815,8 @@ __device__ __forceinline__ void setup_env(
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const int row = 16 * rb + lc;
-        const double h = sHa[(row < NV ? row : 0) * NA + (kv ? k : 0)];
+        const double h = kHaG ? wha[D::W_HD + (row < NV ? row : 0) * NV + (kv ? k : 0)]
+                              : sHa[(row < NV ? row : 0) * NA + (kv ? k : 0)];
         hf[rb][q] = (kv && row < NV) ? h : 0.0;
       }
     }
@@ -806,7 +828,8 @@ __device__ __forceinline__ void setup_env(
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int row = 16 * rb + lg + 4 * rr, col = 16 * cb + lc;
-          const double f = sHa[(row < NV ? row : 0) * NA + NV];
+          const double f = kHaG ? wha[D::W_GD + (row < NV ? row : 0)]
+                                : sHa[(row < NV ? row : 0) * NA + NV];
           t1[rb][cb][rr] = (row < NV && col == NY) ? f : 0.0;
         }
 #pragma unroll
@@ -899,13 +922,16 @@ __device__ __forceinline__ void setup_env(
 #ifndef OSC_SETUP_WPS
 #define OSC_SETUP_WPS 2
 #endif
+#ifndef OSC_SETUP_LEAN_WPS
+#define OSC_SETUP_LEAN_WPS 4
+#endif
 template <class D, bool LEAN = false>
-__global__ __launch_bounds__(kWave, OSC_SETUP_WPS) void osc_setup_kernel(
+__global__ __launch_bounds__(kWave, LEAN ? OSC_SETUP_LEAN_WPS : OSC_SETUP_WPS) void osc_setup_kernel(
     const DevParams* __restrict__ P, int nenv, const double* __restrict__ gM,
     const double* __restrict__ gC, const double* __restrict__ gJ, const double* __restrict__ gb,
     const double* __restrict__ gT, const double* __restrict__ gmask, double* __restrict__ ws,
     const double* __restrict__ gwd) {
-  __shared__ __attribute__((aligned(16))) double sm[D::SMEM];
+  __shared__ __attribute__((aligned(16))) double sm[(LEAN && !D::WH) ? D::SMEM_L : D::SMEM];
   setup_env<D, false, LEAN>(P, static_cast<int>(blockIdx.x), nenv, gM, gC, gJ, gb, gT, gmask, ws,
                             sm, gwd);
 }
