@@ -175,12 +175,13 @@ struct Dims {
   static constexpr int O_WT = O_WA + NW * WAST;
   static constexpr int WTST = NY + 1;   // the basis rows' LDS stride (odd: no bank conflicts)
   static constexpr int SMEM = O_WT + (WH ? (NW + NY) * WTST : 0);
-  // Lean assembly (large batches, round 6): phase D reads H_dv / f_dv back from the workspace
-  // (phase B stores them there bitwise as it forms them), so Ha needs no LDS at all, and X -- whose
-  // columns phase C computes in registers before storing any -- overlays A (dead once they are
-  // computed): 14.2 -> 7.6 KB for Go2, from 11 to 16 waves per CU (its 100 VGPRs' limit)
+  // Lean assembly (Go2, round 6): Ha is kept as H_dv alone (row stride NV; f_dv, phase D's only
+  // other use of it, comes back from the workspace), and X, whose columns phase C computes in
+  // registers before storing any, overlays A (dead once they are computed): 14.2 -> 10.2 KB for
+  // Go2, from 11 to 16 waves per CU (its 100 VGPRs' limit)
   static constexpr int O_X_L = 0;
-  static constexpr int O_MASK_L = R1 + R2;
+  static constexpr int O_HD_L = R1 + R2;
+  static constexpr int O_MASK_L = O_HD_L + even(NV * NV);
   static constexpr int SMEM_L = O_MASK_L + even(NC);
   static_assert(NV * NY1P <= R1 + R2, "lean assembly: X over A and M");
   static_assert(NW <= kRow, "IPM: one wheel row per lane of the env's row");

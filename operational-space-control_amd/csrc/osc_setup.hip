@@ -8,7 +8,7 @@ namespace osc {
 // one env per 64-lane wavefront (four envs per wavefront measured no faster: Go2 4,096
 // 35.3 vs 33.7 us)
 // (the models without MFMA assembly -- Go2 -- take the lean variant, osc_setup.hpp setup_env's
-// LEAN, at every batch size: 100 VGPRs and 7.6 KB of LDS fit all of 4,096 envs' waves at once;
+// LEAN, at every batch size: 100 VGPRs and 10.2 KB of LDS fit all of 4,096 envs' waves at once;
 // against the full variant 4,096 / 2,048 -1.8 / -0.1 %, profiles/r06/lean_lds/)
 template <class D>
 void launch_setup(const LaunchArgs& a) {

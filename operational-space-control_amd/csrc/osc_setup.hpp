@@ -108,10 +108,10 @@ __device__ __noinline__ void wave_mgs_lds(double* rows, int lane, double drop, d
 // kinematics' model tables and per-env state live in the region phases B-D use later (from
 // D::O_HA), so the fused kernel needs kin_lds_doubles<D>() of LDS.
 // LEAN = true (Go2's launches, osc_setup.hip): phase B's 2x2-tile loop unrolled 4 deep instead of
-// fully -- 100 VGPRs instead of 256 -- and (kHaG below) Ha kept out of LDS and X laid over A: 7.6
-// instead of 14.2 KB, so 20 waves fit a CU.  Round 5 adopted the unroll for batches past one round
-// of interior-point waves only (4,096: 0.1646 vs 0.1620 ms, when LDS still capped a CU at 11
-// waves; profiles/r05/ab_setup_unroll4.jsonl); with the LDS cut it wins at every size
+// fully -- 100 VGPRs instead of 256 -- and (kHaG below) only H_dv kept of Ha and X laid over A:
+// 10.2 instead of 14.2 KB of LDS, so 16 waves fit a CU.  Round 5 adopted the unroll for batches
+// past one round of interior-point waves only (4,096: 0.1646 vs 0.1620 ms, when LDS still capped
+// a CU at 11 waves; profiles/r05/ab_setup_unroll4.jsonl); with the LDS cut it wins at every size
 // (profiles/r06/lean_lds/).
 template <class D, bool KIN = false, bool LEAN = false>
 __device__ __forceinline__ void setup_env(
@@ -130,9 +130,9 @@ __device__ __forceinline__ void setup_env(
   double* sA = sm + D::O_A;
   double* sM = sm + D::O_M;
   double* sC = sm + D::O_C;
-  // lean assembly without wheel rows: X in Ha's region, phase D's H_dv / f_dv from the workspace
+  // lean assembly without wheel rows: X over A, H_dv alone in LDS (osc_device.hpp Dims::SMEM_L)
   constexpr bool kHaG = LEAN && !D::WH && !KIN;
-  double* sHa = sm + D::O_HA;
+  double* sHa = sm + (kHaG ? D::O_HD_L : D::O_HA);
   double* sX = sm + (kHaG ? D::O_X_L : D::O_X);
   double* sU = sX + NB * NY1P;   // U parked in X's last rows until X replaces it
   double* sMask = sm + (kHaG ? D::O_MASK_L : D::O_MASK);
@@ -348,7 +348,12 @@ __device__ __forceinline__ void setup_env(
     if (i >= NA || j >= NA) return;
     v *= 2.0;
     if (i == j && i < NV) v += 2.0 * P->w_reg;
-    if constexpr (!kHaG) {   // (the lean assembly reads H_dv / f_dv back from the workspace)
+    if constexpr (kHaG) {   // H_dv alone, row stride NV
+      if (j < NV) {
+        sHa[i * NV + j] = v;
+        sHa[j * NV + i] = v;
+      }
+    } else {
       sHa[i * NA + j] = v;
       sHa[j * NA + i] = v;
     }
@@ -788,8 +793,8 @@ __device__ __forceinline__ void setup_env(
   STAMP_END(2);
   STAMP_BEGIN();
   // ---------------- Phase D: reduced Hessian / gradient ----------------------------------
-  // (kHaG: H_dv / f_dv come back from the workspace -- this wavefront's own stores of phase B,
-  // complete and visible to its loads after a workgroup-scope fence)
+  // (kHaG: f_dv comes back from the workspace -- this wavefront's own stores of phase B, complete
+  // and visible to its loads after a workgroup-scope fence)
   if constexpr (kHaG) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   // Hr = X' T1 + 2 (w_tau + w_reg) I_u + 2 w_reg I_z,  g = last column,  T1 = H_dv X (+ f_dv in
   // the affine column).
@@ -815,8 +820,8 @@ __device__ __forceinline__ void setup_env(
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const int row = 16 * rb + lc;
-        const double h = kHaG ? wha[D::W_HD + (row < NV ? row : 0) * NV + (kv ? k : 0)]
-                              : sHa[(row < NV ? row : 0) * NA + (kv ? k : 0)];
+        const int hr = row < NV ? row : 0, hk = kv ? k : 0;
+        const double h = sHa[hr * (kHaG ? NV : NA) + hk];
         hf[rb][q] = (kv && row < NV) ? h : 0.0;
       }
     }
