@@ -245,12 +245,12 @@ constexpr bool hr_fits_lds() {   // four one-wave workgroups per CU, 160 KB of L
 struct ParkArgs {
   int32_t* list;    // [nenv]  env of each parked slot
   int32_t* count;   // parked envs (zeroed before the park pass)
-  double* park;     // [nenv][park_doubles<D>()]  y (32) | s | lambda | rp (NRL x 16 each)
+  double* park;     // [nenv][park_doubles<D>()]  y (32) | s | lambda | rp (NRL x 16 each) | rd (32)
   int park_it;      // iteration at whose top the park pass parks
 };
 constexpr int kCpNone = 0, kCpPark = 1, kCpResume = 2;
 template <class D>
-constexpr int park_doubles() { return 2 * kRow + 3 * D::NRL * kRow; }
+constexpr int park_doubles() { return 4 * kRow + 3 * D::NRL * kRow; }
 
 // Upper-triangle pair tables (i <= j), built at compile time.
 template <int N, bool SKIP_CORNER>

@@ -756,6 +756,16 @@ __device__ __forceinline__ void ipm_block(
   double rp[NRL];
 #pragma unroll
   for (int t = 0; t < NRL; ++t) rp[t] = 0.0;
+  // The dual residual rd = Hr y + g + G'lam is carried the same way (round 6): with the Newton
+  // system K dy = G'w - rd solved, Hr dy + G'dlam = G'w - rd - G'DG dy + G'(-w + DG dy) = -rd,
+  // so the step leaves (1 - alpha) rd -- up to the solve's rounding, which is why it is formed
+  // from scratch (Hr y by DPP broadcasts, G'lam from LDS: 8 % of an iteration) whenever rp is:
+  // at iteration 0, after a re-centring and once mu <= 1e-6.  Per env (an env's rd never depends
+  // on its wave-mates'); a wave forms it only when one of its running envs needs it.  (Not with
+  // wheel rows: their rd lives in rotated coordinates.)
+  constexpr bool kRdCarry = !D::WH;
+  double rdc0 = 0.0, rdc1 = 0.0;
+  bool rd_fresh = true, rd_have = false;   // (rd_have: a compaction's resume pass starts mid-solve)
   // Warm start (the reference's OsqpSolver::SetWarmStart, operational_space_controller.h:525):
   // an env whose warm state is valid starts from the previous tick's y and lambda, with the
   // slacks s = max(h - G y, delta) and lambda = max(lambda_prev, delta) (rows active now but not
@@ -793,6 +803,9 @@ __device__ __forceinline__ void ipm_block(
         lam[t] = pk[2 * kRow + NRL * kRow + l + kRow * t];
         rp[t] = pk[2 * kRow + 2 * NRL * kRow + l + kRow * t];
       }
+      rdc0 = pk[2 * kRow + 3 * NRL * kRow + l];
+      rdc1 = pk[3 * kRow + 3 * NRL * kRow + l];
+      rd_have = true;
       sVy[j0] = y0;
       if (v1) sVy[j1] = y1;
       wave_sync();
@@ -928,6 +941,7 @@ __device__ __forceinline__ void ipm_block(
       for (int t = 0; t < NRL; ++t) cs += act[t] ? s[t] * lam[t] : 0.0;
       mu = row_sum(cs) / fmax(m_act, 1.0);
       const bool fresh = it == 0 || mu <= 1e-6 || restart;
+      rd_fresh = fresh || !rd_have;
       if (__ballot(fresh) != 0) {   // wave-uniform
         wave_sync();
 #pragma unroll
@@ -958,6 +972,8 @@ __device__ __forceinline__ void ipm_block(
               pk[2 * kRow + NRL * kRow + l + kRow * t] = lam[t];
               pk[2 * kRow + 2 * NRL * kRow + l + kRow * t] = rp[t];
             }
+            pk[2 * kRow + 3 * NRL * kRow + l] = rdc0;
+            pk[3 * kRow + 3 * NRL * kRow + l] = rdc1;
             if (l == 0) PA.list[slot] = env;
             parked = true;
             done = true;
@@ -982,21 +998,27 @@ __device__ __forceinline__ void ipm_block(
     STAMP_END(1);
     STAMP_BEGIN();
     // ---- Newton matrix K = Hr + G' D G (columns j0, j1 in registers) and rd = Hr y + g + G'lam
-    double rd0, rd1;
-    GTw2(sVr, rd0, rd1);
-    if constexpr (WHR) rot_in(rd0, rd1, rd0, rd1);   // T'G'lam
-    rd0 += g0;
-    rd1 += g1;
-    double dg0 = hdg0, dg1 = hdg1;
-    if constexpr (WHR) {   // rd^ += H^ y^
-      if (!init) {
-        double yh0, yh1;
-        rot_in(y0, y1, yh0, yh1);
-        dot_rows<NY>(rd0, rd1, yh0, yh1, c0, c1);
+    double rd0 = rdc0, rd1 = rdc1;
+    if (!kRdCarry || init || __ballot(rd_fresh && !done) != 0) {   // (wave-uniform)
+      double rn0, rn1;
+      GTw2(sVr, rn0, rn1);
+      if constexpr (WHR) rot_in(rn0, rn1, rn0, rn1);   // T'G'lam
+      rn0 += g0;
+      rn1 += g1;
+      if constexpr (WHR) {   // rd^ += H^ y^
+        if (!init) {
+          double yh0, yh1;
+          rot_in(y0, y1, yh0, yh1);
+          dot_rows<NY>(rn0, rn1, yh0, yh1, c0, c1);
+        }
+      } else {
+        if (!init) dot_rows<NY>(rn0, rn1, y0, y1, c0, c1);    // rd += Hr y (y broadcast by DPP)
       }
-    } else {
-      if (!init) dot_rows<NY>(rd0, rd1, y0, y1, c0, c1);    // rd += Hr y (y broadcast by DPP)
+      rd0 = (!kRdCarry || rd_fresh) ? rn0 : rd0;
+      rd1 = (!kRdCarry || rd_fresh) ? rn1 : rd1;
     }
+    rd_have = true;
+    double dg0 = hdg0, dg1 = hdg1;
     STAMP_END(8);
     STAMP_BEGIN();
     // G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
@@ -1161,6 +1183,10 @@ __device__ __forceinline__ void ipm_block(
         s[t] = act[t] ? fma(alpha, ds[t], s[t]) : 1.0;
         lam[t] = act[t] ? fma(alpha, dl[t], lam[t]) : 0.0;
         rp[t] *= 1.0 - alpha;
+      }
+      if constexpr (kRdCarry) {
+        rdc0 = (1.0 - alpha) * rd0;
+        rdc1 = (1.0 - alpha) * rd1;
       }
     }
     sVy[j0] = y0;
