@@ -334,6 +334,56 @@ __device__ __forceinline__ double keep_lanes(double v) {
   }
 }
 
+// The same selects on a lane mask formed by a VALU compare of the lane's index in its row (l)
+// against K straight into VCC: three issue slots (v_cmp, two v_cndmask) where the SGPR-literal
+// mask takes five or six (two s_mov, an s_nop the SALU -> VALU mask read needs on gfx950, two
+// v_cndmask).  A wavefront alone on its SIMD pays ~4.5 clocks for EVERY instruction it issues,
+// scalar ones and s_nop included (tools/mb/mb_issue.hip, profiles/r06/issue/), which is the
+// interior point's situation at 4,096 envs.  Volatile: the triangular solves place them between
+// the DPP FMAs on purpose -- their three VALU instructions are the two wait states the next DPP
+// read of a just-written value needs, so those FMAs carry no s_nop of their own.
+// sel_eq: `set` on the lane l == K of each row, `clear` elsewhere.
+// (the compare is an asm statement of its own: hipcc pads any inline asm that reads a register
+// the previous inline asm wrote with an s_nop -- gfx950's conservative forwarding-hazard rule for
+// asm producers -- so the compare, which reads only l, goes between the DPP FMA that wrote `set`
+// and the selects that read it)
+template <int K>
+__device__ __forceinline__ unsigned long long lane_eq(int l) {
+  unsigned long long m;
+  asm volatile("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m) : "n"(K), "v"(l));
+  return m;
+}
+template <int K>
+__device__ __forceinline__ unsigned long long lane_gt(int l) {
+  unsigned long long m;
+  asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "n"(K), "v"(l));
+  return m;
+}
+__device__ __forceinline__ double sel_mask(unsigned long long m, double set, double clear) {
+  int lo, hi;
+  asm volatile("v_cndmask_b32_e64 %0, %2, %3, %6\n\t"
+               "v_cndmask_b32_e64 %1, %4, %5, %6"
+               : "=&v"(lo), "=v"(hi)
+               : "v"(__double2loint(clear)), "v"(__double2loint(set)), "v"(__double2hiint(clear)),
+                 "v"(__double2hiint(set)), "s"(m));
+  return __hiloint2double(hi, lo);
+}
+template <int K>
+__device__ __forceinline__ double sel_eq(int l, double set, double clear) {
+  return sel_mask(lane_eq<K>(l), set, clear);
+}
+// keep_gt: v on the lanes l > K of each row, +0.0 elsewhere.
+template <int K>
+__device__ __forceinline__ double keep_gt(int l, double v) {
+  const unsigned long long m = lane_gt<K>(l);
+  int lo, hi;
+  asm volatile("v_cndmask_b32_e64 %0, 0, %2, %4\n\t"
+               "v_cndmask_b32_e64 %1, 0, %3, %4"
+               : "=&v"(lo), "=v"(hi)
+               : "v"(__double2loint(v)), "v"(__double2hiint(v)), "s"(m));
+  return __hiloint2double(hi, lo);
+}
+
 // Broadcast lane K of each 16-lane row to the whole row: v_mov_b64_dpp row_newbcast:K.
 template <int K>
 __device__ __forceinline__ double rowb(double v) {

@@ -77,9 +77,11 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
     sdinv[k] = inv;
     c0[k] = -c0[k] * inv;
     c1[k] = -c1[k] * inv;
-    t0 = keep_lanes<rows_mask(lanes_from(k + 1, 15))>(c0[k]);
-    constexpr unsigned kT1 = (k < kRow) ? 0xFFFFu : lanes_from(k + 1 - kRow, N - 1 - kRow);
-    t1 = keep_lanes<rows_mask(kT1)>(c1[k]);
+    // (lanes l > k by a compare on the lane index, osc_device.hpp keep_gt; in slot 1 the mirror
+    // lanes past N keep their multipliers too and so stay exact copies of column N - 1)
+    t0 = keep_gt<k>(l, c0[k]);
+    if constexpr (k < kRow) t1 = c1[k];
+    else t1 = keep_gt<k - kRow>(l, c1[k]);
   };
   // one trailing FMA pair of step k, row i (NOP: the DPP source was written just before)
   auto upd = [&](auto kc, auto ic, double t0, double t1) {
@@ -131,16 +133,15 @@ __device__ __forceinline__ void ldl_fwd_rows(const double (&c0)[N], const double
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    constexpr unsigned long long kPiv = rows_mask(1u << kl);
     if constexpr (s == 0) {
-      z0 = select_lanes<kPiv>(a0, z0);
+      z0 = sel_eq<kl>(l, a0, z0);   // (its three VALU instructions: the DPP read's wait states)
       const double p = a0;
-      fmac_bcast<kl, true>(a1, p, c1[k]);
+      fmac_bcast<kl>(a1, p, c1[k]);
       if constexpr (k < kRow - 1) fmac_bcast<kl>(a0, p, c0[k]);
     } else {
-      z1 = select_lanes<kPiv>(a1, z1);
+      z1 = sel_eq<kl>(l, a1, z1);
       const double p = a1;
-      fmac_bcast<kl, true>(a1, p, c1[k]);
+      fmac_bcast<kl>(a1, p, c1[k]);
     }
   });
   a0 = z0;
@@ -154,15 +155,14 @@ __device__ __forceinline__ void ldl_bwd_rows(const double (&c0)[N], const double
   static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    constexpr unsigned long long kPiv = rows_mask(1u << kl);
     if constexpr (s == 0) {
-      x0 = select_lanes<kPiv>(a0, x0);
+      x0 = sel_eq<kl>(l, a0, x0);
       const double p = a0;
-      if constexpr (k >= 1) fmac_bcast<kl, true>(a0, p, c0[k]);
+      if constexpr (k >= 1) fmac_bcast<kl>(a0, p, c0[k]);
     } else {
-      x1 = select_lanes<kPiv>(a1, x1);
+      x1 = sel_eq<kl>(l, a1, x1);
       const double p = a1;
-      fmac_bcast<kl, true>(a0, p, c0[k]);
+      fmac_bcast<kl>(a0, p, c0[k]);
       if constexpr (k > kRow) fmac_bcast<kl>(a1, p, c1[k]);
     }
   });
