@@ -6,6 +6,7 @@
 // osc_ipm_wheels.hip) so the three compile in parallel.
 #pragma once
 #include "osc_internal.hpp"
+#include "osc_ipm_asm.hpp"
 
 namespace osc {
 
@@ -30,6 +31,12 @@ template <int N>
 __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double x1,
                                          const double (&ma)[N], const double (&mb)[N]) {
   double a2 = 0.0, b2 = 0.0;                // two chains: no back-to-back dependent f64 ops
+  if constexpr (N == 24 || N == 32) {       // one asm statement (osc_ipm_asm.hpp): no s_nop per pair
+    dot_rows_asm<N>(a, b, a2, b2, x0, x1, ma, mb);
+    a += a2;
+    b += b2;
+    return;
+  }
   static_for<0, N>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     if constexpr (i % 2 == 0)
@@ -130,6 +137,12 @@ __device__ __forceinline__ void ldl_fwd_rows(const double (&c0)[N], const double
                                              double dinv0, double dinv1,
                                              double& a0, double& a1, int l) {
   double z0 = 0.0, z1 = 0.0;                // z_j, saved at step j
+  if constexpr (N == 24 || N == 32) {       // one asm statement (osc_ipm_asm.hpp), bitwise the same
+    ldl_fwd_asm<N>(c0, c1, a0, a1, z0, z1, l);
+    a0 = z0;
+    a1 = z1;
+    return;
+  }
   static_for<0, N>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
@@ -152,6 +165,12 @@ __device__ __forceinline__ void ldl_bwd_rows(const double (&c0)[N], const double
                                              double dinv0, double dinv1,
                                              double& a0, double& a1, int l) {
   double x0 = 0.0, x1 = 0.0;                // D-scaled x_j, saved at step j
+  if constexpr (N == 24 || N == 32) {
+    ldl_bwd_asm<N>(c0, c1, a0, a1, x0, x1, l);
+    a0 = x0 * dinv0;
+    a1 = x1 * dinv1;
+    return;
+  }
   static_for<0, N>([&](auto kc) {
     constexpr int k = N - 1 - decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;

@@ -29,7 +29,8 @@ ARCH = os.environ.get("OSC_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["osc_ipm_go2.hip", "osc_ipm_walter.hip", "osc_ipm_wheels.hip", "osc_multi.hip",
            "osc_setup.hip", "osc_gi.hip", "osc_dual.hip", "osc_kinematics.hip",
            "osc_producers.hip", "osc_api.hip", "osc_model.cpp", "osc_mjcf.cpp", "osc_host_feed.cpp"]
-HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp", "osc_kin_device.hpp",
+HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp", "osc_ipm_asm.hpp",
+           "osc_kin_device.hpp",
            "osc_qpos.hpp", "osc_wave_sum.hpp"]
 # device-code units, for the static checks that read the generated assembly
 DEVICE_SOURCES = [s for s in SOURCES if s.endswith(".hip")]
