@@ -71,7 +71,10 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // first, its step k riding along the factor's -- measured within noise: Go2 4,096 0.1739 vs
 // 0.1718 ms per solve, 65,536 1.760 vs 1.748, WaLTER 4,096 0.2754 vs 0.2768, and not bitwise;
 // profiles/r04k/ab_fwd_fused.jsonl.)
-template <int N>
+// ASM: the scheduled one-statement form (osc_ipm_asm.hpp) -- it claims 12 VGPRs of its own, which
+// the one-wave kernels (512 registers with the AGPRs) have to spare and the two-wave ones do not
+// (their spills grow 12 -> 52 bytes per lane), so those keep the per-pivot form.
+template <int N, bool ASM = true>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1) {
   // pivot k's preparation: -> (t0, t1) = -L[lane][k] for the lanes still to be eliminated
@@ -102,6 +105,18 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
       fmac_bcast_self<kl, nop>(c1[i], t1);
     }
   };
+  if constexpr (ASM && (N == 24 || N == 32)) {
+    // one scheduled asm statement (tools/gen_ipm_asm.py -> osc_ipm_asm.hpp): the same
+    // instructions on the same values, pivot k+1's preparation interleaved with pivot k's FMAs
+    // so that the FMAs are the wait states (no s_nop, no asm-boundary padding)
+    const unsigned addr = static_cast<unsigned>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) double*)sdinv));
+    ldl_asm<N>(c0, c1, thr0, thr1, l, addr);
+    wave_sync();
+    dinv0 = sdinv[l];
+    dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
+    return;
+  }
   double ta0, ta1;
   prep(std::integral_constant<int, 0>{}, ta0, ta1);
   static_for<0, N>([&](auto kc) {
@@ -1078,7 +1093,7 @@ __device__ __forceinline__ void ipm_block(
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
-    ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+    ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
     wave_sync();
     STAMP_END(3);
 
@@ -1418,7 +1433,7 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         wave_sync();
-        ldl_rows<NY>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+        ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
         if constexpr (kXinHr) {
           if (round == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X has landed
         }
