@@ -74,14 +74,19 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // ASM: the scheduled one-statement form (osc_ipm_asm.hpp) -- it claims 12 VGPRs of its own, which
 // the one-wave kernels (512 registers with the AGPRs) have to spare and the two-wave ones do not
 // (their spills grow 12 -> 52 bytes per lane), so those keep the per-pivot form.
+// du: the torque rows' diagonal terms of G'DG (lane q's column q < NU, 0 on the other lanes),
+// added to each pivot where it is taken (round 6: the diagonal of K enters the factorisation only
+// as its pivots, so the same K as adding du to c0[l] up front -- which took a lane select per torque
+// column every iteration -- up to the rounding of the pivots' sums)
 template <int N, bool ASM = true>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
-                                         double& dinv0, double& dinv1, double thr0, double thr1) {
+                                         double& dinv0, double& dinv1, double thr0, double thr1,
+                                         double du) {
   // pivot k's preparation: -> (t0, t1) = -L[lane][k] for the lanes still to be eliminated
   auto prep = [&](auto kc, double& t0, double& t1) {
     constexpr int k = decltype(kc)::value;
     constexpr int s = k / kRow, kl = k % kRow;
-    const double own = (s == 0) ? c0[k] : c1[k];
+    const double own = (s == 0) ? c0[k] + du : c1[k];
     const double dk = bcast_guarded<kl>(own > ((s == 0) ? thr0 : thr1) ? own : 1e128);
     const double inv = recip1(dk);
     sdinv[k] = inv;
@@ -111,7 +116,7 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
     // so that the FMAs are the wait states (no s_nop, no asm-boundary padding)
     const unsigned addr = static_cast<unsigned>(
         reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) double*)sdinv));
-    ldl_asm<N>(c0, c1, thr0, thr1, l, addr);
+    ldl_asm<N>(c0, c1, thr0, thr1, l, addr, du);
     wave_sync();
     dinv0 = sdinv[l];
     dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
@@ -1052,7 +1057,7 @@ __device__ __forceinline__ void ipm_block(
       rd1 = (!kRdCarry || rd_fresh) ? rn1 : rd1;
     }
     rd_have = true;
-    double dg0 = hdg0, dg1 = hdg1;
+    double dg0 = hdg0, dg1 = hdg1, du = 0.0;
     STAMP_END(8);
     STAMP_BEGIN();
     // G_u' D G_u is diagonal, d_q = D[2q] + D[2q+1] on (q, q): lane q's column j0 = q
@@ -1061,12 +1066,8 @@ __device__ __forceinline__ void ipm_block(
     } else {
       static_assert(D::NU <= kRow, "torque variables in the first column slot");
       const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
-      const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
+      du = (j0 < NU) ? dd.x + dd.y : 0.0;   // (added to the pivots by ldl_rows)
       dg0 += du;
-      static_for<0, NU>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        c0[i] += keep_lanes<rows_mask(1u << i)>(du);
-      });
     }
     STAMP_END(9);
     STAMP_BEGIN();
@@ -1093,7 +1094,7 @@ __device__ __forceinline__ void ipm_block(
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
-    ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+    ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1, du);
     wave_sync();
     STAMP_END(3);
 
@@ -1343,18 +1344,14 @@ __device__ __forceinline__ void ipm_block(
         if (v1) sVy[j1] = y1;
         wave_sync();
         // K_A in c0 / c1 (they hold Hr's columns)
-        double dg0 = hdg0, dg1 = hdg1;
+        double dg0 = hdg0, dg1 = hdg1, du = 0.0;
         if constexpr (WHR) {
           wave_sync();
           assemble_rot(dg0, dg1);
         } else {
           const double2 dd = *reinterpret_cast<const double2*>(sDr + 2 * (j0 < NU ? j0 : 0));
-          const double du = (j0 < NU) ? dd.x + dd.y : 0.0;
+          du = (j0 < NU) ? dd.x + dd.y : 0.0;
           dg0 += du;
-          static_for<0, NU>([&](auto I) {
-            constexpr int i = decltype(I)::value;
-            c0[i] += keep_lanes<rows_mask(1u << i)>(du);
-          });
         }
         if (!WHR && jk0 >= 0) {
           double a, b, cc;
@@ -1433,7 +1430,7 @@ __device__ __forceinline__ void ipm_block(
           }
         }
         wave_sync();
-        ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1);
+        ldl_rows<NY, SMALL>(c0, c1, B + LY::I_DINV, l, dinv0, dinv1, 1e-13 * dg0, 1e-13 * dg1, du);
         if constexpr (kXinHr) {
           if (round == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X has landed
         }

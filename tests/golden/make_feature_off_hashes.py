@@ -16,7 +16,8 @@ stops (Go2 eps_mu 1e-6, WaLTER 1e-8) and the multipliers of rows leaving the ref
 set zeroed.  Regenerated once in round 5 (profiles/run_r05h.sh) for the
 refinement's one-change rounds (the most violated row joins, else the most negative multiplier
 leaves: tests/golden/go2_unrefined_joint_states.npz).  Regenerated once in round 6 for the
-interior point's carried dual residual (rd formed from scratch only where rp is: DESIGN.md §3.2).
+interior point's carried dual residual (rd formed from scratch only where rp is: DESIGN.md §3.2), and again for the torque rows'
+diagonal terms added to the pivots inside the factorisation.
 Regenerate
 only for an intentional numerical change of the default kernels, and say so in the commit.
 """

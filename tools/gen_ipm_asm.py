@@ -153,7 +153,7 @@ __device__ __forceinline__ void ldl_bwd_asm(const double (&c0)[N], const double 
 // LDL^T in place (osc_ipm.hpp ldl_rows<N, true>): 1 / D_k to LDS at byte address addr + 8 k
 template <int N>
 __device__ __forceinline__ void ldl_asm(double (&c0)[N], double (&c1)[N], double thr0, double thr1,
-                                        int l, unsigned addr);
+                                        int l, unsigned addr, double du);
 // a += sum_i bcast(x_i) ma[i] over the even i, a2 over the odd ones (b, b2 with mb)
 template <int N>
 __device__ __forceinline__ void dot_rows_asm(double& a, double& b, double& a2, double& b2,
@@ -203,7 +203,10 @@ def ldl_prep(k, n):
     G, D, R = SCR["G"], SCR["D"], SCR["R"]
     S = f"S{k % 2}"
     Sr = SCR[S]
-    p = [Ins(f"v_mov_b64 v[{G}:{G + 1}], {r64(own)}", w=["G"], r=[own]),
+    # slot 0: the pivot gets the torque rows' diagonal term du (osc_ipm.hpp ldl_rows)
+    first = (Ins(f"v_add_f64 v[{G}:{G + 1}], {r64(own)}, %[du]", w=["G"], r=[own, "du"]) if s == 0
+             else Ins(f"v_mov_b64 v[{G}:{G + 1}], {r64(own)}", w=["G"], r=[own]))
+    p = [first,
          Ins(f"v_cmp_gt_f64 vcc, v[{G}:{G + 1}], %[{thr}]", r=["G", thr], wvcc=True),
          Ins(f"v_cndmask_b32 v{G}, v{SCR['B']}, v{G}, vcc", w=["G"], r=["G", "B"], rvcc=True),
          Ins(f"v_cndmask_b32 v{G + 1}, v{SCR['B'] + 1}, v{G + 1}, vcc", w=["G"], r=["G", "B"], rvcc=True),
@@ -317,11 +320,11 @@ def emit_ldl(n):
     return f"""// N = {n}: LDL^T, {sum(1 for t in ins if not t.startswith("s_nop"))} instructions, {sum(int(t.split()[1]) + 1 for t in ins if t.startswith("s_nop"))} wait slots
 template <>
 __device__ __forceinline__ void ldl_asm<{n}>(double (&c0)[{n}], double (&c1)[{n}], double thr0,
-                                           double thr1, int l, unsigned addr) {{
+                                           double thr1, int l, unsigned addr, double du) {{
   asm volatile(
 {asm_text(ins)}
       : {outs}
-      : [thr0] "v"(thr0), [thr1] "v"(thr1), [l] "v"(l), [addr] "v"(addr)
+      : [thr0] "v"(thr0), [thr1] "v"(thr1), [l] "v"(l), [addr] "v"(addr), [du] "v"(du)
       : "vcc", "memory", {clob});
 }}
 """
