@@ -334,6 +334,15 @@ __device__ __forceinline__ double keep_lanes(double v) {
   }
 }
 
+// keep_lanes on a mask already in an SGPR pair (one mask_here for several selects)
+__device__ __forceinline__ double keep_m(unsigned long long m, double v) {
+  int lo, hi;
+  asm("v_cndmask_b32_e64 %0, 0, %2, %4\n\tv_cndmask_b32_e64 %1, 0, %3, %4"
+      : "=&v"(lo), "=v"(hi)
+      : "v"(__double2loint(v)), "v"(__double2hiint(v)), "s"(m));
+  return __hiloint2double(hi, lo);
+}
+
 // The same selects on a lane mask formed by a VALU compare of the lane's index in its row (l)
 // against K straight into VCC: three issue slots (v_cmp, two v_cndmask) where the SGPR-literal
 // mask takes five or six (two s_mov, an s_nop the SALU -> VALU mask read needs on gfx950, two
@@ -454,6 +463,12 @@ constexpr int kStampBlocks = 1 << 15;
       for (int q_ = 0; q_ < kStampSlots; ++q_)                               \
         P->setup_stamps[blockIdx.x * kStampSlots + q_] = st_acc[q_];         \
   } while (0)
+#elif defined(OSC_PHASE_MARKS)   // static analysis builds: phase labels in the listing (tools/)
+#define STAMP_DECL
+#define STAMP_BEGIN() asm volatile(";@@BEGIN")
+#define STAMP_END(slot) asm volatile(";@@END " #slot)
+#define STAMP_STORE() do {} while (0)
+#define STAMP_STORE_SETUP() do {} while (0)
 #else
 #define STAMP_DECL
 #define STAMP_BEGIN() do {} while (0)

@@ -649,6 +649,35 @@ __device__ __forceinline__ void ipm_block(
 
   double c0[NY], c1[NY];
   double dinv0, dinv1;
+  // G'DG's contact blocks into K's columns (c0 / c1), row by row (round 6): the rows of contact k
+  // are NU + 3k .. NU + 3k + 2, and the lanes whose column lies in contact k form a compile-time lane
+  // range of each slot -- so each row takes its entry (a, b or cc by the row's component) masked
+  // to that range, and rows no lane of a slot reaches are not touched.  (It was a select per row
+  // of all 12 contact rows against the lane's runtime contact index, behind a branch per slot.)
+  auto add_contact_blocks = [&](double& dg0, double& dg1) __attribute__((always_inline)) {
+    double a0, b0, e0, a1, b1, e1;
+    contact_col(jk0 >= 0 ? jk0 : 0, jc0, a0, b0, e0);
+    contact_col(jk1 >= 0 ? jk1 : 0, jc1, a1, b1, e1);
+    dg0 += jk0 >= 0 ? ((jc0 == 0) ? a0 : (jc0 == 1) ? b0 : e0) : 0.0;
+    dg1 += jk1 >= 0 ? ((jc1 == 0) ? a1 : (jc1 == 1) ? b1 : e1) : 0.0;
+    static_for<0, NC>([&](auto Kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(Kc)::value, r0 = NU + 3 * k;
+      constexpr unsigned m0 = r0 <= kRow - 1 ? lanes_from(r0, r0 + 2) : 0u;   // slot 0: lane = row
+      constexpr unsigned m1 = lanes_from(r0 - kRow, r0 + 2 - kRow);           // slot 1: row - 16
+      if constexpr (m0 != 0u) {
+        const unsigned long long m = mask_here<rows_mask(m0)>();
+        c0[r0] += keep_m(m, a0);
+        c0[r0 + 1] += keep_m(m, b0);
+        c0[r0 + 2] += keep_m(m, e0);
+      }
+      if constexpr (m1 != 0u) {
+        const unsigned long long m = mask_here<rows_mask(m1)>();
+        c1[r0] += keep_m(m, a1);
+        c1[r0 + 1] += keep_m(m, b1);
+        c1[r0 + 2] += keep_m(m, e1);
+      }
+    });
+  };
   // WH: c0 / c1 hold H^'s columns j0, jj1; add T'(G'DG)T from sDr (D per row slot) one original
   // coordinate i at a time -- column j gains coef_i(j) T[i][:], coef_i(j) = (G'DG)[i][:] T[:][j]
   // (torque rows: diagonal; a contact's rows: its 3 x 3 block) -- then pin Q's coordinates.
@@ -1071,26 +1100,7 @@ __device__ __forceinline__ void ipm_block(
     }
     STAMP_END(9);
     STAMP_BEGIN();
-    if (!WHR && jk0 >= 0) {
-      double a, b, cc;
-      contact_col(jk0, jc0, a, b, cc);
-      dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
-#pragma unroll
-      for (int i = NU; i < NY; ++i) {
-        const int ki = (i - NU) / 3, ci = (i - NU) % 3;
-        c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
-      }
-    }
-    if (!WHR && jk1 >= 0) {
-      double a, b, cc;
-      contact_col(jk1, jc1, a, b, cc);
-      dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
-#pragma unroll
-      for (int i = NU; i < NY; ++i) {
-        const int ki = (i - NU) / 3, ci = (i - NU) % 3;
-        c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
-      }
-    }
+    if constexpr (!WHR) add_contact_blocks(dg0, dg1);
     wave_sync();
     STAMP_END(2);
     STAMP_BEGIN();
@@ -1353,26 +1363,7 @@ __device__ __forceinline__ void ipm_block(
           du = (j0 < NU) ? dd.x + dd.y : 0.0;
           dg0 += du;
         }
-        if (!WHR && jk0 >= 0) {
-          double a, b, cc;
-          contact_col(jk0, jc0, a, b, cc);
-          dg0 += (jc0 == 0) ? a : (jc0 == 1) ? b : cc;
-#pragma unroll
-          for (int i = NU; i < NY; ++i) {
-            const int ki = (i - NU) / 3, ci = (i - NU) % 3;
-            c0[i] += (ki == jk0) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
-          }
-        }
-        if (!WHR && jk1 >= 0) {
-          double a, b, cc;
-          contact_col(jk1, jc1, a, b, cc);
-          dg1 += (jc1 == 0) ? a : (jc1 == 1) ? b : cc;
-#pragma unroll
-          for (int i = NU; i < NY; ++i) {
-            const int ki = (i - NU) / 3, ci = (i - NU) % 3;
-            c1[i] += (ki == jk1) ? ((ci == 0) ? a : (ci == 1) ? b : cc) : 0.0;
-          }
-        }
+        if constexpr (!WHR) add_contact_blocks(dg0, dg1);
         // HRL: X is copied global -> LDS by DMA (no registers) into Hr's region -- free now, K_A
         // is in registers -- issued before the factorisation, waited for after it, so its latency
         // hides behind the LDL^T.  A DMA wave-instruction writes 16 B per lane to a wave-uniform
