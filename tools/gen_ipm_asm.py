@@ -134,6 +134,12 @@ __device__ __forceinline__ void dot_rows_asm<{n}>(double& a, double& b, double& 
 
 
 def main():
+    with open(OUT, "w") as f:
+        f.write(render())
+    print(OUT)
+
+
+def render():
     parts = [f"""// osc_ipm_asm.hpp -- GENERATED by tools/gen_ipm_asm.py (do not edit): the interior point's
 // triangular solves and Hr y product, one inline-asm statement each (see the generator's notes).
 // Included by osc_ipm.hpp; N = the reduced QP's size (24: unitree_go2, 32: walter_sr).
@@ -168,9 +174,7 @@ __device__ __forceinline__ void dot_rows_asm(double& a, double& b, double& a2, d
         parts.append(emit_dot(n))
         parts.append(emit_ldl(n))
     parts.append("}  // namespace osc\n")
-    with open(OUT, "w") as f:
-        f.write("\n".join(parts))
-    print(OUT)
+    return "\n".join(parts)
 
 
 
