@@ -10,7 +10,7 @@ intentional change of the LDL factor's storage (row k pre-scaled by -1/D_k, mult
 triangular solves: DESIGN.md §5), and again for the refinement rounds settling per env (an env
 whose round ends without a violation keeps that round's result when a wave-mate asks for another
 round: results no longer depend on which envs share a wavefront); the wheel rows' changes do not
-reach models without them.  Regenerated once in round 4 (profiles/run_r04d.sh) for the
+reach models without them.  Regenerated once in round 4 (profiles/run_r04d.sh, in git history at cfe45c1) for the
 refinement accepted on a KKT test instead of a per-lane move bound, the interior point's earlier
 stops (Go2 eps_mu 1e-6, WaLTER 1e-8) and the multipliers of rows leaving the refinement's active
 set zeroed.  Regenerated once in round 5 (profiles/run_r05h.sh) for the

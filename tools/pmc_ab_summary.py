@@ -1,4 +1,4 @@
-"""Summarise profiles/run_r04n.sh: per interior-point kernel VARIANT (one-wave `<D, true, ...>` vs
+"""Summarise the round-4 variant PMC run (profiles/run_r04n.sh, in git history at cfe45c1): per interior-point kernel VARIANT (one-wave `<D, true, ...>` vs
 two-wave `<D, false, ...>`, told apart by the template arguments of the kernel name), its average
 duration (kernel trace) and per-dispatch PMC counters -- HBM bytes (gfx950: 2 x FETCH_SIZE +
 WRITE_SIZE, KiB; MI355X_MICROARCH.md), the SQ cycle / wait / issue counters and the instruction

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 outputs of profiles/run_r01.sh: per-kernel average duration (kernel
+"""Summarise rocprofv3 outputs of the round-1 profiling run (profiles/run_r01.sh, in git history at cfe45c1): per-kernel average duration (kernel
 trace) and per-dispatch PMC counters, HBM traffic per solve launch (gfx950 FETCH_SIZE doubled,
 MI355X_MICROARCH.md §HBM) and executed FP64 work.  Writes profiles/pmc_traffic.json and
 profiles/<prefix>_counters.json; copies the raw CSVs next to them."""
