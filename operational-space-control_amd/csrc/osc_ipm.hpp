@@ -78,6 +78,12 @@ __device__ __forceinline__ void dot_rows(double& a, double& b, double x0, double
 // added to each pivot where it is taken (round 6: the diagonal of K enters the factorisation only
 // as its pivots, so the same K as adding du to c0[l] up front -- which took a lane select per torque
 // column every iteration -- up to the rounding of the pivots' sums)
+// An empty asm that "rewrites" columns I.. of both slots (ldl_rows: orders their last VALU writes)
+template <int I, int N>
+__device__ __forceinline__ void touch_cols(double (&c0)[N], double (&c1)[N]) {
+  asm volatile("" : "+v"(c0[I]), "+v"(c1[I]));
+  if constexpr (I + 1 < N) touch_cols<I + 1, N>(c0, c1);
+}
 template <int N, bool ASM = true>
 __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], double* sdinv, int l,
                                          double& dinv0, double& dinv1, double thr0, double thr1,
@@ -122,6 +128,11 @@ __device__ __forceinline__ void ldl_rows(double (&c0)[N], double (&c1)[N], doubl
     dinv1 = sdinv[(l + kRow < N) ? l + kRow : N - 1];
     return;
   }
+  // Step 0's DPP reads take columns the caller's C++ just wrote (K = Hr + G'DG): every column goes
+  // through an empty asm first and then one s_nop 1, so no schedule can put a column's VALU write
+  // within the DPP read's two wait states (tests/test_asm_hazards.py; LLVM's ILP scheduler did).
+  touch_cols<0, N>(c0, c1);
+  asm volatile("s_nop 1");
   double ta0, ta1;
   prep(std::integral_constant<int, 0>{}, ta0, ta1);
   static_for<0, N>([&](auto kc) {

@@ -32,6 +32,12 @@ SOURCES = ["osc_ipm_go2.hip", "osc_ipm_walter.hip", "osc_ipm_wheels.hip", "osc_m
 HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp", "osc_ipm_asm.hpp",
            "osc_kin_device.hpp",
            "osc_qpos.hpp", "osc_wave_sum.hpp"]
+# Per-unit compiler flags (variant builds may pass their own map to build()).  The interior-point
+# units use LLVM's iterative ILP scheduler (round 6): bitwise the same results, faster per solve
+# (profiles/r06/sched/); ldl_rows' column barrier keeps its schedule clear of DPP hazards
+# (tests/test_asm_hazards.py compiles with these flags).  Not the assembly's unit: slower with it.
+_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+UNIT_FLAGS: dict = {"osc_ipm_go2.hip": _ILP, "osc_ipm_walter.hip": _ILP, "osc_ipm_wheels.hip": _ILP}
 # device-code units, for the static checks that read the generated assembly
 DEVICE_SOURCES = [s for s in SOURCES if s.endswith(".hip")]
 
@@ -50,7 +56,7 @@ def compile_flags(defines=()) -> list:
 
 
 def build(verbose: bool = False, force: bool = False, out: str | None = None,
-          defines=()) -> str:
+          defines=(), unit_flags: dict | None = None) -> str:
     out = out or OUT
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + \
@@ -72,7 +78,8 @@ def build(verbose: bool = False, force: bool = False, out: str | None = None,
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        cmd = [HIPCC, *flags, "-c", src, "-o", obj]
+        extra = (UNIT_FLAGS if unit_flags is None else unit_flags).get(os.path.basename(src), [])
+        cmd = [HIPCC, *flags, *extra, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

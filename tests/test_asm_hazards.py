@@ -12,6 +12,9 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
+from osc_amd.build import UNIT_FLAGS  # noqa: E402
+
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -23,6 +26,7 @@ def test_no_dpp_hazards_in_kernels(tmp_path, unit):
     out = tmp_path / f"{unit}.s"
     src = os.path.join(REPO, "operational-space-control_amd", "csrc", f"{unit}.hip")
     subprocess.run([HIPCC, "-std=c++17", "-O3", "--offload-arch=gfx950", "--cuda-device-only",
+                    *UNIT_FLAGS.get(f"{unit}.hip", []),   # the flags the product build uses
                     "-S", "-I", os.path.join(REPO, "include"), "-o", str(out), src],
                    check=True, capture_output=True)
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_dpp_hazards.py"),

@@ -12,6 +12,8 @@ import sys
 import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "operational-space-control_amd"))
+from osc_amd.build import UNIT_FLAGS  # noqa: E402
 
 
 def demangle(names):
@@ -27,7 +29,7 @@ def main(argv):
     with tempfile.TemporaryDirectory() as td:
         r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950",
                             "-fPIC", "-c", "--cuda-device-only", "-I", os.path.join(REPO, "include"),
-                            *defs, src, "-o", os.path.join(td, "k.o"),
+                            *defs, *UNIT_FLAGS.get(os.path.basename(src), []), src, "-o", os.path.join(td, "k.o"),
                             "-Rpass-analysis=kernel-resource-usage"],
                            capture_output=True, text=True)
     rows, cur = [], None
