@@ -36,8 +36,11 @@ HEADERS = ["osc_device.hpp", "osc_internal.hpp", "osc_setup.hpp", "osc_ipm.hpp",
 # units use LLVM's iterative ILP scheduler (round 6): bitwise the same results, faster per solve
 # (profiles/r06/sched/); ldl_rows' column barrier keeps its schedule clear of DPP hazards
 # (tests/test_asm_hazards.py compiles with these flags).  Not the assembly's unit: slower with it.
+# The two-model unit (configs[4]'s pair kernels) too: mixed 24.09 -> 24.75 M solves/s, its GPU tests
+# bitwise against the solo solves (profiles/r06/sched/multi/).
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-UNIT_FLAGS: dict = {"osc_ipm_go2.hip": _ILP, "osc_ipm_walter.hip": _ILP, "osc_ipm_wheels.hip": _ILP}
+UNIT_FLAGS: dict = {"osc_ipm_go2.hip": _ILP, "osc_ipm_walter.hip": _ILP, "osc_ipm_wheels.hip": _ILP,
+              "osc_multi.hip": _ILP}
 # device-code units, for the static checks that read the generated assembly
 DEVICE_SOURCES = [s for s in SOURCES if s.endswith(".hip")]
 
